@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Benchmark of the north-star kernel: int4 symmetric group-128 quantize + pack of a synthetic
+bf16 weight [11008, 4096] (BASELINE.json configs[1]: "Qwen3-4B AWQ int4 group_size=128 on
+1xMI355X"; metric "params quantized/sec + achieved HBM GB/s").
+
+One *step* = one fused quantize+pack pass (qz_quantize, one kernel launch) over one
+[11008, 4096] bf16 weight already resident in HBM.  The step rotates over COPIES distinct
+input buffers (> the 256 MiB Infinity Cache) so every step streams its weight from HBM, not L3
+(BASELINE.md timing protocol).  Multi-GPU: one process per GPU, each quantizes its own weight
+shard set (weak scaling, no collective in the timed region); after timing, ranks reassemble
+the packed tensors with one RCCL all-gather (reported separately, as the north star asks).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ROWS, COLS, GROUP, BITS = 11008, 4096, 128, 4
+PARAMS = ROWS * COLS
+# algorithmic bytes per launch: read 2 B/param + packed 0.5 B/param + bf16 scale/group
+ALG_BYTES = PARAMS * 2 + PARAMS * BITS // 8 + (PARAMS // GROUP) * 2  # 113,426,432
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128"
+KERNEL_NAME = "k_group_fast<4, 0, false>"
+
+# Qwen3-4B linear shapes (hidden 2560, inter 9728, 32 q / 8 kv heads x 128), 36 layers
+QWEN3_4B = [("q_proj", 4096, 2560), ("k_proj", 1024, 2560), ("v_proj", 1024, 2560), ("o_proj", 2560, 4096),
+            ("gate_proj", 9728, 2560), ("up_proj", 9728, 2560), ("down_proj", 2560, 9728)]
+QWEN3_LAYERS = 36
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--copies", type=int, default=6)
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-model-pass", action="store_true")
+    p.add_argument("--profile-only", action="store_true",
+                   help="just warmup + K launches (for rocprofv3 runs); prints nothing else")
+    return p.parse_args()
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(seconds: float):
+    """The oracle's torch-op restatement of compressed-tensors (oracle/ct_torch.py), timed on the
+    host cores on the same synthetic weight."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ct_torch as ct  # CPU baseline leg only
+
+    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    w = (torch.randn(ROWS, COLS, generator=g) * 0.02).to(torch.bfloat16)
+    a = ct.QArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
+    ct.compress_weight(w, a)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ct.compress_weight(w, a)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 3) or n >= 1000:
+            break
+    return {"value": n * PARAMS / el, "unit": "params/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ct_torch.compress_weight (compressed-tensors op sequence, torch CPU) on the same "
+                      f"bf16 [{ROWS},{COLS}] int4-g{GROUP} weight, {n} calls in {el:.1f}s, "
+                      f"torch threads={threads}, os.cpu_count()={os.cpu_count()}, cpu='{cpu_model()}'"}
+
+
+def read_pmc_traffic():
+    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), d.get("source")
+    except Exception:
+        return None, None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from quantizers_amd import ops
+    from quantizers_amd.quantization import QuantizationArgs
+
+    a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    copies = [(torch.randn(ROWS, COLS, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+              for _ in range(args.copies)]
+    out = ops.quantize_weight(copies[0], a)  # allocates outputs + workspace
+    bufs = {"codes": out["codes"], "scale": out["scale"], "zero_point": out["zero_point"]}
+    stream = torch.cuda.current_stream(dev)
+    prep = ops.PreparedQuantize(copies[0], a, bufs)
+
+    def step(i):
+        prep.run(copies[i % args.copies], stream)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if args.profile_only:
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize()
+        return
+
+    # ---- contract timing: barrier + sync, exactly K steps, sync + barrier, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = t.item()
+
+    # ---- per-launch kernel duration with HIP events on the launch stream (roofline)
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step(i)
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    durs = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    k_ms_mean = sum(durs) / len(durs)
+    k_ms_med = durs[len(durs) // 2]
+
+    # ---- correctness guard on the measured buffers (bit-exact vs the C oracle on a slice)
+    ok = None
+    if rank == 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import qref  # checker only
+        last = (args.steps - 1) % args.copies
+        ref_p, ref_s = qref.int_sym_group_pack(copies[last][:256].cpu(), BITS, GROUP)
+        ok = bool(torch.equal(bufs["codes"][:256].cpu(), ref_p) and
+                  torch.equal(bufs["scale"][:256].cpu().view(torch.int16), ref_s.view(torch.int16)))
+
+    # ---- reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
+    allgather = None
+    if world > 1:
+        gathered_codes = torch.empty((world,) + tuple(bufs["codes"].shape), dtype=bufs["codes"].dtype, device=dev)
+        gathered_scale = torch.empty((world,) + tuple(bufs["scale"].shape), dtype=bufs["scale"].dtype, device=dev)
+        for _ in range(3):
+            dist.all_gather_into_tensor(gathered_codes, bufs["codes"])
+            dist.all_gather_into_tensor(gathered_scale, bufs["scale"])
+        torch.cuda.synchronize()
+        dist.barrier()
+        ta = time.perf_counter()
+        reps = 10
+        for _ in range(reps):
+            dist.all_gather_into_tensor(gathered_codes, bufs["codes"])
+            dist.all_gather_into_tensor(gathered_scale, bufs["scale"])
+        torch.cuda.synchronize()
+        allgather = (time.perf_counter() - ta) / reps * 1e3
+
+    # ---- whole-model pass: every Qwen3-4B linear (36 layers, batched per shape)
+    model_pass = None
+    if not args.no_model_pass:
+        del copies
+        torch.cuda.empty_cache()
+        ws = []
+        for name, n, k in QWEN3_4B:
+            ws.append((name, (torch.randn(QWEN3_LAYERS, n, k, device=dev, generator=gen) * 0.02).to(torch.bfloat16)))
+        outs = [ops.quantize_weight(w, a) for _, w in ws]  # warm + allocate
+        torch.cuda.synchronize()
+        reps = 5
+        tm = time.perf_counter()
+        for _ in range(reps):
+            for (_, w), o in zip(ws, outs):
+                ops.quantize_weight(w, a, out={"codes": o["codes"], "scale": o["scale"], "zero_point": o["zero_point"]})
+        torch.cuda.synchronize()
+        mp = (time.perf_counter() - tm) / reps
+        nparams = sum(w.numel() for _, w in ws)
+        model_pass = {"params": nparams, "ms": mp * 1e3, "params_per_s": nparams / mp,
+                      "alg_GBps": nparams * (2 + BITS / 8 + 2 / GROUP) / mp / 1e9, "launches": len(ws)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+
+    if rank == 0:
+        ms_step = el / args.steps * 1e3
+        value = world * PARAMS * args.steps / el
+        achieved = ALG_BYTES / (k_ms_mean * 1e-3) / 1e9
+        traffic, tsrc = read_pmc_traffic()
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "params/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic: torch.randn*0.02 bf16 weights (no checkpoint); same shape as Qwen3-4B's 11008x4096",
+            "config": {"workload": f"int4 sym group_size={GROUP} quantize+pack (pack-quantized) of bf16 W[{ROWS},{COLS}]"
+                                   f", {args.copies} rotating HBM-resident copies",
+                       "rows": ROWS, "cols": COLS, "group_size": GROUP, "num_bits": BITS,
+                       "parallelism": f"weight-shard dp{world}"},
+            "hbm_GBps_step": world * ALG_BYTES * args.steps / el / 1e9,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": KERNEL_NAME, "kernel_ms_mean": k_ms_mean, "kernel_ms_median": k_ms_med,
+                         "alg_bytes_per_launch": ALG_BYTES, "traffic_source": tsrc},
+            "cpu_baseline": cpu,
+            "parity_check": ok,
+            "allgather_ms": allgather,
+            "qwen3_4b_all_linears": model_pass,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,204 @@
+/*
+ * quantizers_amd.h -- C ABI of the MI355X (gfx950) weight-quantization library.
+ *
+ * This is the drop-in boundary for the reference's per-linear quantize step.  The reference
+ * (mratsim/quantizers) has no native code and no FFI of its own: the step runs inside
+ * llmcompressor.oneshot(...) (scripts/do_oneshot.py:179-187) and
+ * model.save_pretrained(save_compressed=True) (scripts/do_oneshot.py:197), i.e. in
+ * compressed-tensors' calculate_qparams / quantize / fake_quantize / pack_to_int32 /
+ * pack_fp4_to_uint8 and llmcompressor's AWQ helpers.  Each entry point below names the
+ * reference-side function it replaces; INTEGRATION.md shows the ctypes stub a maintainer would
+ * add.  All buffers are DEVICE pointers owned by the caller; nothing here allocates, frees or
+ * synchronises.  Every call only enqueues work on `stream` (a hipStream_t, NULL = legacy
+ * default stream) and is safe to call from several host threads (one device per thread).
+ *
+ * Weights are bf16 (the dtype do_oneshot.py:88 loads models in), given as a batch of 2-D
+ * slices: element (b, r, c) lives at w[b*ld_batch + r*ld_row + c] (elements, not bytes), so
+ * both per-expert nn.Linear weights and fused [E, N, K] expert parameters are served
+ * (SURVEY.md finding 5).  Outputs are always dense, batch-major.
+ *
+ * Return value: 0 = success; < 0 = argument error (the cases compressed-tensors raises
+ * ValueError for); > 0 = the hipError_t of a failed launch.  qz_strerror() names codes.
+ */
+#ifndef QUANTIZERS_AMD_H
+#define QUANTIZERS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* qz_stream_t; /* hipStream_t */
+
+/* QuantizationArgs.type */
+enum { QZ_INT = 0, QZ_FLOAT = 1 };
+/* QuantizationArgs.strategy */
+enum { QZ_TENSOR = 0, QZ_CHANNEL = 1, QZ_GROUP = 2, QZ_BLOCK = 3, QZ_TENSOR_GROUP = 4 };
+/* scale storage: NATIVE = weight dtype (bf16, decision D3); E4M3 = NVFP4 scale_dtype;
+ * E8M0 = MXFP4 exponent bytes */
+enum { QZ_SCALE_NATIVE = 0, QZ_SCALE_E4M3 = 2, QZ_SCALE_E8M0 = 3 };
+
+/* what qz_quantize writes to q_out (compressed-tensors compression formats) */
+enum {
+  QZ_OUT_PACKED_INT32 = 0, /* pack-quantized: int32 [rows, cols*bits/32], nibble i of word j = col 8j+i (bits=4) */
+  QZ_OUT_INT8 = 1,         /* int-quantized / module weight before packing: int8 [rows, cols] */
+  QZ_OUT_FP8 = 2,          /* float-quantized: float8_e4m3fn bytes [rows, cols] */
+  QZ_OUT_FP4_PACKED = 3,   /* nvfp4/mxfp4-pack-quantized: uint8 [rows, cols/2], even col in low nibble */
+  QZ_OUT_FAKEQUANT = 4     /* fake_quantize: bf16 [rows, cols] = dequantize(quantize(w)) */
+};
+
+/* Mirrors the compressed-tensors QuantizationArgs fields the reference's recipes use
+ * (configs/recipes/recipe_awq_w4a16.yaml:16-24, recipe_mixed_fp8_int4.yaml:9-24,
+ *  recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:24-48, recipe_MoE_RTN_NVFP4.yaml:17-21). */
+typedef struct qz_args {
+  int32_t num_bits;   /* 2..8 int; 8 (e4m3) or 4 (e2m1) float */
+  int32_t type;       /* QZ_INT / QZ_FLOAT */
+  int32_t symmetric;  /* 1 / 0 (float requires 1) */
+  int32_t strategy;   /* QZ_TENSOR .. QZ_TENSOR_GROUP */
+  int32_t group_size; /* GROUP / TENSOR_GROUP */
+  int32_t block_h;    /* BLOCK: block_structure[0] */
+  int32_t block_w;    /* BLOCK: block_structure[1] */
+  int32_t scale_fmt;  /* QZ_SCALE_* */
+} qz_args;
+
+/* Error codes */
+enum {
+  QZ_OK = 0,
+  QZ_ERR_NULL = -1,         /* a required pointer is NULL */
+  QZ_ERR_SHAPE = -2,        /* negative / zero-sized dims where not allowed */
+  QZ_ERR_GROUP = -3,        /* cols % group_size != 0 ("tensor column shape must be divisible by group_size") */
+  QZ_ERR_BLOCK = -4,        /* rows/cols not divisible by block ("Block quantization requires exact division") */
+  QZ_ERR_BITS = -5,         /* num_bits unsupported for type / output format */
+  QZ_ERR_ASYM_FLOAT = -6,   /* "Asymmetric Quantization is not supported for FP4/FP8" */
+  QZ_ERR_FORMAT = -7,       /* output format incompatible with args */
+  QZ_ERR_WORKSPACE = -8,    /* workspace smaller than qz_quantize_workspace_size() */
+  QZ_ERR_ALIGN = -9         /* pointer/ld alignment violated where required */
+};
+
+const char* qz_strerror(int code);
+int qz_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */
+
+/* Bytes of device workspace qz_quantize / qz_fake_quantize need for these args (0 for the
+ * single-pass group path).  The workspace needs no initialisation. */
+size_t qz_quantize_workspace_size(int64_t batch, int64_t rows, int64_t cols, const qz_args* a);
+
+/*
+ * qz_quantize -- memoryless observe + calculate_qparams + quantize (+ pack), one weight batch.
+ * Replaces, per targeted Linear: the memoryless_minmax weight observer -> calculate_qparams
+ * ([3P] compressed-tensors, called from llmcompressor during oneshot, do_oneshot.py:179) and
+ * the compressor's quantize(..., dtype=int8) -> pack_to_int32 / float8 cast /
+ * pack_fp4_to_uint8 (save_pretrained(save_compressed=True), do_oneshot.py:197).
+ *   scale_out : bf16 / e4m3 / e8m0 per group; shape [batch][groups] where groups is
+ *               rows*cols/g (GROUP, TENSOR_GROUP), rows (CHANNEL), 1 (TENSOR),
+ *               (rows/bh)*(cols/bw) (BLOCK)
+ *   zp_out    : int8 per group (may be NULL; written as 0 for symmetric)
+ *   gscale_out: f32 [batch] NVFP4 global scale (TENSOR_GROUP only; otherwise may be NULL)
+ */
+int qz_quantize(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
+                int64_t ld_batch, const qz_args* a, int32_t out_fmt, void* q_out,
+                void* scale_out, int8_t* zp_out, float* gscale_out, void* workspace,
+                size_t workspace_bytes, qz_stream_t stream);
+
+/*
+ * qz_quantize_qparams -- quantize with caller-supplied qparams (stateful observers such as the
+ * recipes' `minmax`, recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:48).  Replaces [3P]
+ * compressed-tensors quantize(x, scale, zero_point, args) / fake_quantize(...).
+ * scale/zp/gscale have the qz_quantize output layouts; zp may be NULL for symmetric.
+ */
+int qz_quantize_qparams(const void* w, int64_t batch, int64_t rows, int64_t cols,
+                        int64_t ld_row, int64_t ld_batch, const qz_args* a, int32_t out_fmt,
+                        const void* scale, const int8_t* zp, const float* gscale, void* q_out,
+                        qz_stream_t stream);
+
+/*
+ * qz_observe_minmax -- per-group amin/amax of the weight in bf16 (exact), the observation
+ * step of [3P] llmcompressor's observers (flatten_for_calibration + amin/amax).  Outputs
+ * are bf16 [batch][groups] (TENSOR_GROUP -> GROUP layout).
+ */
+int qz_observe_minmax(const void* w, int64_t batch, int64_t rows, int64_t cols,
+                      int64_t ld_row, int64_t ld_batch, const qz_args* a, void* min_out,
+                      void* max_out, void* workspace, size_t workspace_bytes,
+                      qz_stream_t stream);
+
+/*
+ * qz_calculate_qparams -- [3P] compressed-tensors calculate_qparams(min, max, args,
+ * global_scale) over n groups given bf16 min/max.  gscale (f32, may be NULL) is one value
+ * for all n groups.
+ */
+int qz_calculate_qparams(const void* min_vals, const void* max_vals, int64_t n,
+                         const qz_args* a, const float* gscale, void* scale_out,
+                         int8_t* zp_out, qz_stream_t stream);
+
+/*
+ * qz_dequantize -- [3P] compressed-tensors dequantize / the decompressors: codes in the
+ * qz_quantize q_out layout (PACKED_INT32, INT8, FP8, FP4_PACKED) -> bf16 [batch][rows][cols].
+ */
+int qz_dequantize(const void* q, int64_t batch, int64_t rows, int64_t cols, const qz_args* a,
+                  int32_t in_fmt, const void* scale, const int8_t* zp, const float* gscale,
+                  void* w_out, qz_stream_t stream);
+
+/*
+ * qz_pack_int32 -- [3P] compressed-tensors pack_to_int32(value, num_bits, packed_dim):
+ * int8 [rows, cols] -> int32 [rows, ceil(cols*bits/32)] (packed_dim 1) or
+ * [ceil(rows*bits/32), cols] (packed_dim 0, the asymmetric weight_zero_point layout).
+ */
+int qz_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int32_t num_bits,
+                  int32_t packed_dim, int32_t* out, qz_stream_t stream);
+
+/* ---------------------------------------------------------------- AWQ */
+
+/*
+ * qz_awq_absmean_accum -- adds sum_t |x[t, c]| (fp32, decision D8) into sum[c] for a bf16
+ * activation block x [tokens, channels] (row stride ld).  Replaces the running mean|x| of
+ * [3P] llmcompressor AWQModifier's cache_smooth_activations_hook (_accumulate_mean).
+ * Deterministic: fixed-order two-stage reduction through `workspace`
+ * (qz_awq_absmean_workspace_size bytes).
+ */
+size_t qz_awq_absmean_workspace_size(int64_t tokens, int64_t channels);
+int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_t ld,
+                         float* sum, void* workspace, size_t workspace_bytes,
+                         qz_stream_t stream);
+
+/*
+ * qz_awq_weight_mean_accum -- adds sum_r |W[r,c]| / (absmax(group(r,c)) + 1e-6) (bf16
+ * elementwise, fp64 sum) into wsum[c] for one balance layer W [rows, cols].  group_size =
+ * the layer's quantization group (cols for channel strategy).  Replaces [3P] llmcompressor
+ * _compute_layer_means.
+ */
+int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld,
+                             int32_t group_size, double* wsum, qz_stream_t stream);
+
+/*
+ * qz_awq_grid_scales -- one grid point of [3P] AWQModifier._compute_best_scale (fp32):
+ * s = clamp(x_mean^r / (w_mean^(1-r) + 1e-4), 1e-4) (duo) or clamp(x_mean^r, 1e-4);
+ * s /= sqrt(max(s) * min(s)); inf/nan -> 1.  Single workgroup; channels <= 65536.
+ */
+int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channels,
+                       float ratio, int32_t duo_scaling, float* scales_out,
+                       qz_stream_t stream);
+
+/*
+ * qz_awq_fake_quant -- the grid search's per-balance-layer step W' = Q(W * s) / s with the
+ * layer's own scheme, fused into one pass (bf16 products, bf16 fake-quant, f32 column
+ * scales).  col_scales may be NULL (plain fake_quantize).  w_out may alias w.
+ */
+int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
+                      int64_t ld_batch, const qz_args* a, const float* col_scales, void* w_out,
+                      void* workspace, size_t workspace_bytes, qz_stream_t stream);
+
+/*
+ * qz_scale_columns / qz_scale_rows -- AWQ _apply_smoothing: in place, bf16-rounded,
+ * W[:, c] *= s[c] (balance layers) or W[r, :] /= s[r] (smooth Linear's last rows; a 1-D norm
+ * weight is rows=n, cols=1).  divide=1 divides, 0 multiplies.
+ */
+int qz_scale_columns(void* w, int64_t rows, int64_t cols, int64_t ld, const float* s,
+                     int32_t divide, qz_stream_t stream);
+int qz_scale_rows(void* w, int64_t rows, int64_t cols, int64_t ld, const float* s,
+                  int32_t divide, qz_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QUANTIZERS_AMD_H */

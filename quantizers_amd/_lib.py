@@ -1,0 +1,93 @@
+"""ctypes binding of the C ABI in include/quantizers_amd.h (libquantizers_amd.so, gfx950).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C quantizers_amd/csrc``).
+There is no CPU fallback: if the shared object is missing or fails to load, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libquantizers_amd.so")
+
+# enums (include/quantizers_amd.h)
+QZ_INT, QZ_FLOAT = 0, 1
+QZ_TENSOR, QZ_CHANNEL, QZ_GROUP, QZ_BLOCK, QZ_TENSOR_GROUP = 0, 1, 2, 3, 4
+QZ_SCALE_NATIVE, QZ_SCALE_E4M3, QZ_SCALE_E8M0 = 0, 2, 3
+QZ_OUT_PACKED_INT32, QZ_OUT_INT8, QZ_OUT_FP8, QZ_OUT_FP4_PACKED, QZ_OUT_FAKEQUANT = 0, 1, 2, 3, 4
+
+QZ_ERR_NULL, QZ_ERR_SHAPE, QZ_ERR_GROUP, QZ_ERR_BLOCK = -1, -2, -3, -4
+QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT, QZ_ERR_WORKSPACE, QZ_ERR_ALIGN = -5, -6, -7, -8, -9
+
+# every symbol the header declares (tests check the library exports all of them)
+EXPORTS = (
+    "qz_strerror", "qz_version", "qz_quantize_workspace_size", "qz_quantize", "qz_quantize_qparams",
+    "qz_observe_minmax", "qz_calculate_qparams", "qz_dequantize", "qz_pack_int32",
+    "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_accum",
+    "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
+)
+
+
+class QzArgs(ctypes.Structure):
+    """``qz_args`` (mirrors compressed-tensors QuantizationArgs fields)."""
+
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("num_bits", "type", "symmetric", "strategy", "group_size", "block_h", "block_w", "scale_fmt")]
+
+
+class QzError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library; raise loudly if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise QzError(f"{LIB_PATH} not built; run __graft_entry__.build() or make -C quantizers_amd/csrc")
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I64, I32, SZ = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_size_t
+    A = ctypes.POINTER(QzArgs)
+    sig = {
+        "qz_strerror": ([ctypes.c_int], ctypes.c_char_p),
+        "qz_version": ([], ctypes.c_int),
+        "qz_quantize_workspace_size": ([I64, I64, I64, A], SZ),
+        "qz_quantize": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P, SZ, P], ctypes.c_int),
+        "qz_quantize_qparams": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P], ctypes.c_int),
+        "qz_observe_minmax": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
+        "qz_calculate_qparams": ([P, P, I64, A, P, P, P, P], ctypes.c_int),
+        "qz_dequantize": ([P, I64, I64, I64, A, I32, P, P, P, P, P], ctypes.c_int),
+        "qz_pack_int32": ([P, I64, I64, I32, I32, P, P], ctypes.c_int),
+        "qz_awq_absmean_workspace_size": ([I64, I64], SZ),
+        "qz_awq_absmean_accum": ([P, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
+        "qz_awq_weight_mean_accum": ([P, I64, I64, I64, I32, P, P], ctypes.c_int),
+        "qz_awq_grid_scales": ([P, P, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
+        "qz_awq_fake_quant": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
+        "qz_scale_columns": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
+        "qz_scale_rows": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
+    }
+    for name, (argtypes, restype) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = restype
+    _lib = lib
+    return lib
+
+
+_VALUE_ERRORS = {QZ_ERR_SHAPE, QZ_ERR_GROUP, QZ_ERR_BLOCK, QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT,
+                 QZ_ERR_ALIGN}
+
+
+def check(rc: int, what: str = "") -> None:
+    """Map C-ABI return codes to the reference's exception types (ValueError for bad args)."""
+    if rc == 0:
+        return
+    msg = load().qz_strerror(rc).decode()
+    if rc in _VALUE_ERRORS:
+        raise ValueError(f"{what}: {msg}")
+    raise QzError(f"{what}: {msg} (code {rc})")

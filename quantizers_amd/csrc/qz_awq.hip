@@ -1,0 +1,274 @@
+// qz_awq.hip -- AWQ statistics, grid-scale and smoothing kernels (gfx950).
+//
+// Replaces the elementwise/reduction parts of [3P] llmcompressor AWQModifier (SURVEY.md §8a
+// a3, a4, a5 scale computation, a6): the per-channel mean|x| hook, the per-channel mean of
+// group-normalised |W| (w_mean), the grid's scale vector and _apply_smoothing.  The
+// fake-quant step of the grid search lives in qz_quant.hip (qz_awq_fake_quant); the parent
+// forwards are PyTorch GEMMs on the host side.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "qz_device.h"
+
+using namespace qz;
+
+namespace {
+
+constexpr int WAVE = 64;
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline bool aligned(const void* p, size_t n) { return ((uintptr_t)p % n) == 0; }
+int launch_err() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QZ_OK : (int)e;
+}
+
+// ---------------------------------------------------------- a3: sum_t |x[t, c]|
+// stage 1: block (256 threads) = 256 channel octets x one token chunk -> partial[chunk][c]
+__global__ __launch_bounds__(256) void k_absmean_partial_v8(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                                            int64_t tc, float* part) {
+  const int64_t c8 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c8 * 8 >= C) return;
+  const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t t = t0; t < t1; ++t) {
+    const uint4 v = *reinterpret_cast<const uint4*>(x + t * ld + c8 * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += fabsf(__uint_as_float(w[k] << 16));
+      acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
+    }
+  }
+  float* dst = part + (int64_t)blockIdx.y * C + c8 * 8;
+  *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+__global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                                            int64_t tc, float* part) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
+  float acc = 0.f;
+  for (int64_t t = t0; t < t1; ++t) acc += fabsf(bf2f(x[t * ld + c]));
+  part[(int64_t)blockIdx.y * C + c] = acc;
+}
+// stage 2: fixed-order sum over chunks, accumulated into sum[c]
+__global__ void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float acc = 0.f;
+  for (int64_t k = 0; k < nch; ++k) acc += part[k * C + c];
+  sum[c] += acc;
+}
+
+int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
+  const int64_t bx = cdiv(C, 2048);
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 16), cdiv(2048, bx)));
+  *tc = cdiv(T, nch);
+  return cdiv(T, *tc);
+}
+
+// ------------------------------------------------- a4: w_mean numerator (f64 sums)
+// block = 4 waves over one 512-column window x a chunk of rows; lane owns 8 columns.
+template <int LOGL>
+__global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t rc,
+                                                  double* wsum) {
+  constexpr int L = 1 << LOGL;
+  __shared__ double red[4][512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 512 + lane * 8;
+  const bool in = c0 < C;
+  const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = r0 + wv; r < r1; r += 4) {
+    uint4 v = in ? *reinterpret_cast<const uint4*>(w + r * ld + c0) : make_uint4(0, 0, 0, 0);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    float a[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[2 * k] = fabsf(__uint_as_float(u[k] << 16));
+      a[2 * k + 1] = fabsf(__uint_as_float(u[k] & 0xffff0000u));
+    }
+    float m = a[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) m = fmaxf(m, a[i]);
+#pragma unroll
+    for (int s = 1; s < L; s <<= 1) m = fmaxf(m, __shfl_xor(m, s, WAVE));
+    const float d = bfr(m + 1e-6f);  // amax + 1e-6 in bf16
+    const float rd = __builtin_amdgcn_rcpf(d);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += (double)bfr(a[i] * rd);  // bf16(|w| / d)
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    const int64_t c = (int64_t)blockIdx.x * 512 + j;
+    if (c < C) {
+      const double s = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+      atomicAdd(&wsum[c], s);
+    }
+  }
+}
+// generic: thread per (row, group) element run; any group size / alignment
+__global__ void k_wmean_generic(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t g, double* wsum) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int64_t gc0 = (c / g) * g;
+  double acc = 0.0;
+  for (int64_t r = 0; r < R; ++r) {
+    float m = 0.f;
+    for (int64_t k = 0; k < g; ++k) m = fmaxf(m, fabsf(bf2f(w[r * ld + gc0 + k])));
+    const float d = bfr(m + 1e-6f);
+    acc += (double)bfr(fabsf(bf2f(w[r * ld + c])) / d);
+  }
+  atomicAdd(&wsum[c], acc);
+}
+
+// ------------------------------------------------------- a5: one grid point's scales
+__device__ __forceinline__ float nmax(float a, float b) { return (a != a || b != b) ? NAN : fmaxf(a, b); }
+__device__ __forceinline__ float nmin(float a, float b) { return (a != a || b != b) ? NAN : fminf(a, b); }
+
+__global__ __launch_bounds__(1024) void k_grid_scales(const float* xm, const float* wm, int64_t C, float ratio,
+                                                      int duo, float* out) {
+  __shared__ float smx[16], smn[16];
+  float lmx = -INFINITY, lmn = INFINITY;
+  for (int64_t c = threadIdx.x; c < C; c += 1024) {
+    float s = powf(xm[c], ratio);
+    if (duo) s = s / (powf(wm[c], 1.0f - ratio) + 1e-4f);
+    s = (s != s) ? s : fmaxf(s, 1e-4f);  // clamp(min=1e-4), NaN propagates
+    out[c] = s;
+    lmx = nmax(lmx, s);
+    lmn = nmin(lmn, s);
+  }
+  for (int m = 1; m < 64; m <<= 1) {
+    lmx = nmax(lmx, __shfl_xor(lmx, m, WAVE));
+    lmn = nmin(lmn, __shfl_xor(lmn, m, WAVE));
+  }
+  if ((threadIdx.x & 63) == 0) { smx[threadIdx.x >> 6] = lmx; smn[threadIdx.x >> 6] = lmn; }
+  __syncthreads();
+  float gmx = smx[0], gmn = smn[0];
+  for (int k = 1; k < 16; ++k) { gmx = nmax(gmx, smx[k]); gmn = nmin(gmn, smn[k]); }
+  const float norm = sqrtf(gmx * gmn);
+  for (int64_t c = threadIdx.x; c < C; c += 1024) {
+    float s = out[c] / norm;
+    if (s != s || fabsf(s) == INFINITY) s = 1.0f;
+    out[c] = s;
+  }
+}
+
+// --------------------------------------------------------------- a6: smoothing
+__global__ void k_scale_cols(uint16_t* w, int64_t R, int64_t C, int64_t ld, const float* s, int divide) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= R * C) return;
+  const int64_t r = e / C, c = e % C;
+  uint16_t* p = w + r * ld + c;
+  const float x = bf2f(*p);
+  *p = f2bf(divide ? x / s[c] : x * s[c]);
+}
+__global__ void k_scale_rows(uint16_t* w, int64_t R, int64_t C, int64_t ld, const float* s, int divide) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= R * C) return;
+  const int64_t r = e / C, c = e % C;
+  uint16_t* p = w + r * ld + c;
+  const float x = bf2f(*p);
+  *p = f2bf(divide ? x / s[r] : x * s[r]);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t qz_awq_absmean_workspace_size(int64_t tokens, int64_t channels) {
+  if (tokens <= 0 || channels <= 0) return 0;
+  int64_t tc;
+  const int64_t nch = absmean_chunks(tokens, channels, &tc);
+  return (size_t)4 * (size_t)(nch * channels);
+}
+
+int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_t ld, float* sum, void* workspace,
+                         size_t workspace_bytes, qz_stream_t stream) {
+  if (!x || !sum) return QZ_ERR_NULL;
+  if (tokens < 0 || channels <= 0 || ld < channels) return QZ_ERR_SHAPE;
+  if (tokens == 0) return QZ_OK;
+  if (!workspace || workspace_bytes < qz_awq_absmean_workspace_size(tokens, channels)) return QZ_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  int64_t tc;
+  const int64_t nch = absmean_chunks(tokens, channels, &tc);
+  float* part = (float*)workspace;
+  const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16);
+  if (v8) {
+    dim3 grid((unsigned)cdiv(channels / 8, 256), (unsigned)nch);
+    hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(256), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
+  } else {
+    dim3 grid((unsigned)cdiv(channels, 256), (unsigned)nch);
+    hipLaunchKernelGGL(k_absmean_partial_v1, grid, dim3(256), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
+  }
+  int rc = launch_err();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 256)), dim3(256), 0, st, part, nch, channels, sum);
+  return launch_err();
+}
+
+int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld, int32_t group_size, double* wsum,
+                             qz_stream_t stream) {
+  if (!w || !wsum) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
+  if (group_size <= 0 || cols % group_size) return QZ_ERR_GROUP;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t g = group_size;
+  const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
+  if (pow2 && ld % 8 == 0 && aligned(w, 16)) {
+    const int64_t bx = cdiv(cols, 512);
+    const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(rows, 16), cdiv(1024, bx)));
+    const int64_t rc = cdiv(rows, nrc);
+    dim3 grid((unsigned)bx, (unsigned)cdiv(rows, rc));
+    int logl = 0;
+    while ((8 << logl) < g) ++logl;
+    const uint16_t* wp = (const uint16_t*)w;
+    switch (logl) {
+      case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 1: hipLaunchKernelGGL(k_wmean_v8<1>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 2: hipLaunchKernelGGL(k_wmean_v8<2>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 3: hipLaunchKernelGGL(k_wmean_v8<3>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 4: hipLaunchKernelGGL(k_wmean_v8<4>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 5: hipLaunchKernelGGL(k_wmean_v8<5>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      default: hipLaunchKernelGGL(k_wmean_v8<6>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+    }
+  } else {
+    hipLaunchKernelGGL(k_wmean_generic, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const uint16_t*)w, rows,
+                       cols, ld, g, wsum);
+  }
+  return launch_err();
+}
+
+int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channels, float ratio, int32_t duo_scaling,
+                       float* scales_out, qz_stream_t stream) {
+  if (!x_mean || !scales_out || (duo_scaling && !w_mean)) return QZ_ERR_NULL;
+  if (channels <= 0 || channels > 65536) return QZ_ERR_SHAPE;
+  hipLaunchKernelGGL(k_grid_scales, dim3(1), dim3(1024), 0, (hipStream_t)stream, x_mean, w_mean, channels, ratio,
+                     (int)duo_scaling, scales_out);
+  return launch_err();
+}
+
+int qz_scale_columns(void* w, int64_t rows, int64_t cols, int64_t ld, const float* s, int32_t divide,
+                     qz_stream_t stream) {
+  if (!w || !s) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
+  hipLaunchKernelGGL(k_scale_cols, dim3((unsigned)cdiv(rows * cols, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (uint16_t*)w, rows, cols, ld, s, (int)divide);
+  return launch_err();
+}
+
+int qz_scale_rows(void* w, int64_t rows, int64_t cols, int64_t ld, const float* s, int32_t divide,
+                  qz_stream_t stream) {
+  if (!w || !s) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
+  hipLaunchKernelGGL(k_scale_rows, dim3((unsigned)cdiv(rows * cols, 256)), dim3(256), 0, (hipStream_t)stream,
+                     (uint16_t*)w, rows, cols, ld, s, (int)divide);
+  return launch_err();
+}
+
+}  // extern "C"

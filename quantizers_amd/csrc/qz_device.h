@@ -1,0 +1,243 @@
+// qz_device.h -- gfx950 device arithmetic shared by the quantize / AWQ kernels.
+//
+// Bit-exactness contract: every value compressed-tensors materialises
+// as a bf16 tensor is rounded here with round-to-nearest-even to bf16 (v_cvt_pk_bf16_f32) at
+// the same point; scalar-by-tensor quotients use IEEE-correct f32 division; per-element
+// bf16/bf16 quotients use x * rcp(s), which is provably equal to bf16(x / s) for 8-bit
+// operands (proof in DESIGN.md §Numerics "rcp lemma", exhaustively tested in
+// tests/test_rcp_lemma.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/quantizers_amd.h"
+
+namespace qz {
+
+// --------------------------------------------------------------------------- kinds
+enum Kind : int { K_INT = 0, K_FP8 = 1, K_MX = 2, K_NV = 3, K_FP4 = 4 };
+
+// Host+device view of the per-call quantization constants.
+struct QP {
+  float qmin, qmax;   // calculate_range
+  float half_range;   // (qmax - qmin) / 2  (symmetric scale divisor)
+  float range;        // qmax - qmin        (asymmetric scale divisor)
+  float magic;        // 2^23 - qmin: t + magic has RNE(t) - qmin in its low mantissa bits
+  int bits;
+  int sym;
+  int kind;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+// round an f32 result to bf16 (RNE, v_cvt_pk_bf16_f32) and widen back
+__device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
+
+// torch.clamp: NaN propagates
+__device__ __forceinline__ float clamp_t(float x, float lo, float hi) {
+  return (x != x) ? x : fminf(fmaxf(x, lo), hi);
+}
+
+// order-preserving float <-> uint32 keys (atomicMin/Max on floats)
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+// ------------------------------------------------------------- float8_e4m3fn (OCP)
+// RNE encode of a finite value with |x| <= 448 given as a bf16 bit pattern.
+__device__ __forceinline__ uint32_t bf16_to_e4m3(uint32_t b) {
+  uint32_t sign = (b >> 8) & 0x80u;
+  uint32_t E = (b >> 7) & 0xffu, m7 = b & 0x7fu;
+  uint32_t code;
+  if (E >= 121u) {  // e4m3 normal range (>= 2^-6)
+    uint32_t v = ((E - 120u) << 7) | m7;
+    v += 0x7u + ((v >> 4) & 1u);
+    code = v >> 4;
+  } else {  // e4m3 subnormal: units of 2^-9
+    uint32_t mant = E ? (128u + m7) : m7;
+    uint32_t sh = E ? (125u - E) : 124u;  // value = mant * 2^(E-134) (E>0) ; units 2^-9
+    if (sh > 24u) sh = 24u;
+    uint32_t half = 1u << (sh - 1u);
+    code = (mant + half - 1u + ((mant >> sh) & 1u)) >> sh;
+  }
+  return sign | code;
+}
+// f32 -> e4m3 for a value that is not necessarily bf16 (NVFP4 scales): RNE, |x| <= 448
+__device__ __forceinline__ uint32_t f32_to_e4m3(float f) {
+  uint32_t u = __float_as_uint(f);
+  uint32_t sign = (u >> 24) & 0x80u;
+  float a = fabsf(f);
+  if (a < 0.015625f) {
+    float n = __builtin_rintf(a * 512.0f);
+    return sign | (uint32_t)n;
+  }
+  uint32_t au = __float_as_uint(a);
+  uint32_t v = ((((au >> 23) & 0xffu) - 120u) << 23) | (au & 0x7fffffu);  // 4-bit exp field
+  v += 0x7ffffu + ((v >> 20) & 1u);
+  return sign | (v >> 20);
+}
+__device__ __forceinline__ float e4m3_to_f32(uint32_t c) {
+  uint32_t s = (c & 0x80u) << 24;
+  uint32_t e = (c >> 3) & 0xfu, m = c & 7u;
+  float v;
+  if (e == 0) v = (float)m * 0.001953125f;  // m * 2^-9
+  else v = __uint_as_float(((e + 120u) << 23) | (m << 20));
+  return __uint_as_float(__float_as_uint(v) | s);
+}
+
+// ------------------------------------------------------------------ FP4 E2M1
+// FP4_E2M1_DATA.cast_to_fp4 thresholds on |x|; sign bit from sign(x) (x<0 -> 0x8, even when
+// the magnitude rounds to 0).
+__device__ __forceinline__ uint32_t fp4_code(float x) {
+  float a = fabsf(x);
+  uint32_t idx = (a > 0.25f) + (a >= 0.75f) + (a > 1.25f) + (a >= 1.75f) + (a > 2.5f) +
+                 (a >= 3.5f) + (a > 5.0f);
+  return idx | ((x < 0.0f) ? 8u : 0u);
+}
+__device__ __forceinline__ float fp4_value(uint32_t code) {
+  const float mag[8] = {0.f, 0.5f, 1.f, 1.5f, 2.f, 3.f, 4.f, 6.f};
+  float v = mag[code & 7u];
+  return (code & 8u) ? -v : v;
+}
+
+// 2^e for e in [-127, 127] (2^-127 is the f32 subnormal 0x00400000)
+__device__ __forceinline__ float mx_pow2(int e) {
+  return e >= -126 ? __uint_as_float((uint32_t)(e + 127) << 23) : __uint_as_float(0x00400000u);
+}
+
+// ------------------------------------------------------------- per-group params
+struct GP {
+  float s;      // dense scale (bf16 value, 2^k for MX, f32 for NV)
+  float rs;     // reciprocal used by the per-element fast quotient
+  float zp;     // zero point as float (exact integer)
+  uint32_t sbits;  // stored scale bits (bf16 / e4m3 / e8m0)
+  bool fast;    // x * rs is exact-equivalent (see header)
+};
+
+// calculate_qparams for one group from its observed min/max (bf16 values as f32).
+// gs: NVFP4 global scale (K_NV only).
+__device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, float gs) {
+  GP g;
+  float lo = fminf(mn, 0.f), hi = fmaxf(mx, 0.f);
+  g.zp = 0.f;
+  if (p.kind == K_MX) {
+    float am = fmaxf(fabsf(lo), fabsf(hi));
+    uint32_t b = f2bf(am);
+    uint32_t e = ((b + 0x40u) >> 7) & 0xffu;  // round_to_power_2 -> exponent field
+    int byte = (int)e - 2;
+    byte = byte < 0 ? 0 : (byte > 254 ? 254 : byte);
+    g.sbits = (uint32_t)byte;
+    // 2^(byte-127) and its reciprocal 2^(127-byte); both f32-representable
+    g.s = mx_pow2(byte - 127);
+    g.rs = mx_pow2(127 - byte);
+    g.fast = true;
+    return g;
+  }
+  float s;
+  if (p.sym) {
+    float am = fmaxf(fabsf(lo), fabsf(hi));
+    s = bfr(am / p.half_range);
+  } else {
+    s = bfr(bfr(hi - lo) / p.range);
+    float t = bfr(lo / s);
+    g.zp = clamp_t(bfr(p.qmin - t), p.qmin, p.qmax);
+    g.zp = (g.zp != g.zp) ? 0.f : __builtin_rintf(g.zp);  // D10: NaN zp -> 0
+  }
+  if (p.kind == K_NV) {
+    float s32 = gs * s;
+    uint32_t s8 = f32_to_e4m3(clamp_t(s32, -448.f, 448.f));
+    float sf = e4m3_to_f32(s8);
+    if (sf == 0.f) { s8 = 0x20u; sf = 0.125f; }  // eps of float8_e4m3fn
+    g.sbits = s8;
+    g.s = sf / gs;  // _quantize: scale / global_scale (f32)
+    g.rs = 0.f;
+    g.fast = false;  // f32 quotient: IEEE division per element
+    return g;
+  }
+  if (s == 0.f) s = 0.0078125f;  // D1: finfo(bf16).eps
+  g.s = s;
+  g.sbits = f2bf(s);
+  g.rs = __builtin_amdgcn_rcpf(s);
+  g.fast = (s >= 0x1.0p-125f) && (s <= 0x1.0p+125f);
+  return g;
+}
+
+// quotient of one element (bf16 value x) by the group scale, as compressed-tensors'
+// `x / scale` (bf16 result; f32 for NVFP4).
+__device__ __forceinline__ float qdiv(const QP& p, const GP& g, float x) {
+  if (p.kind == K_NV) return x / g.s;
+  return bfr(g.fast ? x * g.rs : x / g.s);
+}
+
+// encode: returns the code (int: q - qmin as unsigned; fp8: e4m3 byte; fp4: nibble)
+__device__ __forceinline__ uint32_t encode(const QP& p, const GP& g, float x) {
+  float t = qdiv(p, g, x);
+  if (p.kind == K_INT) {
+    if (!p.sym) t = bfr(t + g.zp);
+    t = clamp_t(t, p.qmin, p.qmax);
+    if (t != t) return (uint32_t)(-(int)p.qmin);  // round(NaN).to(int8) == 0 (D10)
+    return __float_as_uint(t + p.magic) & ((1u << p.bits) - 1u);
+  }
+  if (p.kind == K_FP8) {
+    t = clamp_t(t, -448.f, 448.f);
+    return bf16_to_e4m3(f2bf(t));
+  }
+  t = clamp_t(t, -6.f, 6.f);
+  return fp4_code(t);
+}
+
+// fake-quant of one int element straight from x: torch.round keeps the sign of zero, so a
+// small negative quotient dequantizes to -0 (an int8 code cannot carry that sign)
+__device__ __forceinline__ float fakequant_int(const QP& p, const GP& g, float x) {
+  float t = qdiv(p, g, x);
+  if (!p.sym) t = bfr(t + g.zp);
+  t = clamp_t(t, p.qmin, p.qmax);
+  return bfr(bfr(__builtin_rintf(t) - g.zp) * g.s);
+}
+
+// dequantize one code to the f32 value compressed-tensors' _dequantize produces before the
+// final bf16 cast
+__device__ __forceinline__ float decode(const QP& p, const GP& g, uint32_t code) {
+  if (p.kind == K_INT) {
+    float q = (float)((int)code + (int)p.qmin);
+    return bfr(bfr(q - g.zp) * g.s);
+  }
+  if (p.kind == K_FP8) return bfr(e4m3_to_f32(code) * g.s);
+  if (p.kind == K_NV) return bfr(fp4_value(code) * g.s);
+  return bfr(fp4_value(code) * g.s);
+}
+
+// rebuild GP from stored qparams (qz_quantize_qparams / qz_dequantize)
+__device__ __forceinline__ GP gp_from_stored(const QP& p, int scale_fmt, const void* scale,
+                                              int64_t gi, const int8_t* zp, float gs) {
+  GP g;
+  g.zp = (zp && !p.sym) ? (float)zp[gi] : 0.f;
+  if (p.kind == K_MX) {
+    int byte = ((const uint8_t*)scale)[gi];
+    g.sbits = byte;
+    g.s = mx_pow2(byte - 127);
+    g.rs = mx_pow2(127 - byte);
+    g.fast = true;
+    return g;
+  }
+  if (p.kind == K_NV) {
+    uint32_t s8 = ((const uint8_t*)scale)[gi];
+    g.sbits = s8;
+    g.s = e4m3_to_f32(s8) / gs;
+    g.rs = 0.f;
+    g.fast = false;
+    return g;
+  }
+  uint16_t sb = ((const uint16_t*)scale)[gi];
+  g.sbits = sb;
+  g.s = bf2f(sb);
+  g.rs = __builtin_amdgcn_rcpf(g.s);
+  g.fast = (g.s >= 0x1.0p-125f) && (g.s <= 0x1.0p+125f);
+  return g;
+}
+
+}  // namespace qz

@@ -1,0 +1,790 @@
+// qz_quant.hip -- weight quantize / pack kernels and their C-ABI entry points (gfx950).
+//
+// Two execution paths, identical results (both call qz_device.h's group_params/encode):
+//  * the single-pass GROUP path (k_group_fast): contiguous bf16 weights, group_size = 8*2^k
+//    (8..512).  Each lane owns 8 consecutive elements (one 16-B load); a wave-instruction
+//    reads 1 KiB contiguous, so every load is fully coalesced whatever the row length; the
+//    L = group_size/8 lanes of a group reduce min/max with xor-shuffles; each lane then
+//    writes its 8 codes as one packed word (int4/fp4: 4 B, int8/fp8: 8 B) and the group's
+//    first lane writes the scale.  HBM traffic = read once + write once.
+//  * the generic path (k_minmax_generic -> k_qparams_keys -> k_quant_generic): any
+//    strategy (tensor / channel / block / odd group sizes), strided or unaligned inputs, any
+//    bit width; two reads of the weight.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "qz_device.h"
+
+using namespace qz;
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int BLOCK = 256;
+constexpr int UNROLL = 4;  // 16-B loads in flight per lane
+
+// ------------------------------------------------------------------------ helpers
+__device__ __forceinline__ void unpack8(const uint4& v, float* x) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[2 * k] = __uint_as_float(w[k] << 16);
+    x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+template <int L>
+__device__ __forceinline__ float grp_max(float v) {
+#pragma unroll
+  for (int m = 1; m < L; m <<= 1) v = fmaxf(v, __shfl_xor(v, m, WAVE));
+  return v;
+}
+template <int L>
+__device__ __forceinline__ float grp_min(float v) {
+#pragma unroll
+  for (int m = 1; m < L; m <<= 1) v = fminf(v, __shfl_xor(v, m, WAVE));
+  return v;
+}
+
+struct FastArgs {
+  const uint16_t* w;
+  int64_t n_units;          // batch*rows*cols/8
+  int64_t units_per_batch;  // rows*cols/8
+  int64_t units_per_row;    // cols/8
+  QP p;
+  int out_fmt;
+  int scale_bytes;  // 2 (bf16) or 1 (e4m3 / e8m0)
+  void* q_out;
+  void* s_out;
+  int8_t* zp_out;
+  const float* gscale;      // [batch], NVFP4
+  const float* col_scales;  // [cols], AWQ prescale (FQ only)
+};
+
+// --------------------------------------------------------------- single-pass path
+template <int LOGL, int KIND, bool FQ>
+__global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
+  constexpr int L = 1 << LOGL;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t wave = (int64_t)blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+  const int64_t base = wave * (UNROLL * WAVE);
+  QP p = A.p;
+  p.kind = KIND;
+
+  uint4 v[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t unit = base + u * WAVE + lane;
+    v[u] = unit < A.n_units ? *reinterpret_cast<const uint4*>(A.w + unit * 8) : make_uint4(0, 0, 0, 0);
+  }
+
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t unit = base + u * WAVE + lane;
+    const bool valid = unit < A.n_units;  // uniform within a group (groups never straddle)
+    float x[8];
+    unpack8(v[u], x);
+    float cs[8];
+    if (FQ && A.col_scales) {
+      const int64_t c0 = (unit % A.units_per_row) * 8;
+      const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
+      const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
+      cs[0] = c_lo.x; cs[1] = c_lo.y; cs[2] = c_lo.z; cs[3] = c_lo.w;
+      cs[4] = c_hi.x; cs[5] = c_hi.y; cs[6] = c_hi.z; cs[7] = c_hi.w;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = bfr(x[i] * cs[i]);  // W * s in the weight dtype
+    }
+
+    // ---- observe: memoryless min/max over the group (exact in bf16)
+    float mn, mx;
+    if (p.sym) {
+      float am = fabsf(x[0]);
+#pragma unroll
+      for (int i = 1; i < 8; ++i) am = fmaxf(am, fabsf(x[i]));
+      am = grp_max<L>(am);
+      mn = -am;
+      mx = am;
+    } else {
+      mn = x[0];
+      mx = x[0];
+#pragma unroll
+      for (int i = 1; i < 8; ++i) { mn = fminf(mn, x[i]); mx = fmaxf(mx, x[i]); }
+      mn = grp_min<L>(mn);
+      mx = grp_max<L>(mx);
+    }
+    float gs = 0.f;
+    if (KIND == K_NV) gs = A.gscale[valid ? unit / A.units_per_batch : 0];
+    const GP g = group_params(p, mn, mx, gs);
+
+    // ---- quotient x / scale (bf16; f32 for NVFP4)
+    float t[8];
+    if (KIND == K_NV) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = x[i] / g.s;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = x[i] * g.rs;
+      if (__builtin_expect(!g.fast, 0)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t[i] = x[i] / g.s;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = bfr(t[i]);
+    }
+
+    // ---- round / clamp / encode
+    uint32_t c[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float ti = t[i];
+      if (KIND == K_INT) {
+        if (!p.sym) ti = bfr(ti + g.zp);
+        ti = clamp_t(ti, p.qmin, p.qmax);
+        t[i] = ti;  // kept for fake-quant: round() keeps the sign of zero
+        c[i] = (ti != ti) ? (uint32_t)(-(int)p.qmin)
+                          : (__float_as_uint(ti + p.magic) & ((1u << p.bits) - 1u));
+      } else if (KIND == K_FP8) {
+        c[i] = bf16_to_e4m3(f2bf(clamp_t(ti, -448.f, 448.f)));
+      } else {
+        c[i] = fp4_code(clamp_t(ti, -6.f, 6.f));
+      }
+    }
+
+    if (!valid) continue;
+    if (FQ) {
+      float d[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        d[i] = (KIND == K_INT) ? bfr(bfr(__builtin_rintf(t[i]) - g.zp) * g.s) : decode(p, g, c[i]);
+        if (A.col_scales) d[i] = bfr(d[i] / cs[i]);
+      }
+      uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
+      reinterpret_cast<uint4*>(A.q_out)[unit] = o;
+    } else if (KIND == K_INT && A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) word |= c[i] << (4 * i);
+      reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
+    } else if (KIND == K_INT && A.out_fmt == QZ_OUT_PACKED_INT32) {  // 8 bits: 2 words
+      uint2 o = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                           c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+      reinterpret_cast<uint2*>(A.q_out)[unit] = o;
+    } else if (KIND == K_INT || KIND == K_FP8) {  // int8 / e4m3 bytes
+      uint32_t off = (KIND == K_INT) ? (uint32_t)(-(int)p.qmin) : 0u;
+      uint32_t b[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = (c[i] - off) & 0xffu;
+      uint2 o = make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
+                           b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
+      reinterpret_cast<uint2*>(A.q_out)[unit] = o;
+    } else {  // fp4 packed: element 2k in the low nibble of byte k
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) word |= c[i] << (4 * i);
+      reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
+    }
+    if ((lane & (L - 1)) == 0) {
+      const int64_t gi = unit >> LOGL;
+      if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
+      else reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
+      if (A.zp_out) A.zp_out[gi] = (int8_t)g.zp;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ generic path
+struct GenArgs {
+  const uint16_t* w;
+  int64_t batch, rows, cols, ld_row, ld_batch;
+  int strategy;
+  int64_t g;       // group size (GROUP / TENSOR_GROUP)
+  int64_t bh, bw;  // BLOCK
+  int64_t ng_item; // groups per batch item
+  const float* col_scales;
+};
+
+__device__ __forceinline__ int64_t group_of(const GenArgs& A, int64_t r, int64_t c) {
+  switch (A.strategy) {
+    case QZ_TENSOR: return 0;
+    case QZ_CHANNEL: return r;
+    case QZ_BLOCK: return (r / A.bh) * (A.cols / A.bw) + c / A.bw;
+    default: return r * (A.cols / A.g) + c / A.g;
+  }
+}
+
+__device__ __forceinline__ float load_w(const GenArgs& A, int64_t b, int64_t r, int64_t c) {
+  float x = bf2f(A.w[b * A.ld_batch + r * A.ld_row + c]);
+  if (A.col_scales) x = bfr(x * A.col_scales[c]);
+  return x;
+}
+
+__global__ void k_fill_u32(uint32_t* p, int64_t n, uint32_t v) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+// one workgroup per (group, split): reduce the group's region, merge with key atomics
+__global__ __launch_bounds__(BLOCK) void k_minmax_generic(GenArgs A, uint32_t* kmin, uint32_t* kmax) {
+  const int64_t gi = blockIdx.x;  // global group id
+  const int64_t b = gi / A.ng_item, gl = gi % A.ng_item;
+  int64_t r0, r1, c0, c1;
+  switch (A.strategy) {
+    case QZ_TENSOR: {
+      const int64_t ny = gridDim.y;
+      r0 = A.rows * blockIdx.y / ny;
+      r1 = A.rows * (blockIdx.y + 1) / ny;
+      c0 = 0; c1 = A.cols;
+      break;
+    }
+    case QZ_CHANNEL: r0 = gl; r1 = gl + 1; c0 = 0; c1 = A.cols; break;
+    case QZ_BLOCK: {
+      const int64_t nbc = A.cols / A.bw;
+      r0 = (gl / nbc) * A.bh; r1 = r0 + A.bh;
+      c0 = (gl % nbc) * A.bw; c1 = c0 + A.bw;
+      break;
+    }
+    default: {
+      const int64_t gpr = A.cols / A.g;
+      r0 = gl / gpr; r1 = r0 + 1;
+      c0 = (gl % gpr) * A.g; c1 = c0 + A.g;
+    }
+  }
+  float mn = INFINITY, mx = -INFINITY;
+  const int64_t width = c1 - c0;
+  const int64_t n = (r1 - r0) * width;
+  for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+    const int64_t r = r0 + i / width, c = c0 + i % width;
+    const float x = load_w(A, b, r, c);
+    mn = fminf(mn, x);
+    mx = fmaxf(mx, x);
+  }
+  mn = grp_min<WAVE>(mn);
+  mx = grp_max<WAVE>(mx);
+  __shared__ float smn[BLOCK / WAVE], smx[BLOCK / WAVE];
+  if ((threadIdx.x & 63) == 0) { smn[threadIdx.x >> 6] = mn; smx[threadIdx.x >> 6] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < BLOCK / WAVE; ++k) { mn = fminf(mn, smn[k]); mx = fmaxf(mx, smx[k]); }
+    if (n > 0) {
+      atomicMin(&kmin[gi], f2key(mn));
+      atomicMax(&kmax[gi], f2key(mx));
+    }
+  }
+}
+
+// NVFP4 global scale per batch item: (448*6)/absmax in bf16 as reciprocal-then-multiply
+// (python-scalar / tensor == tensor.reciprocal() * scalar), then widened to f32.
+__global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_t batch, float* gs) {
+  int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= batch) return;
+  float lo = fminf(key2f(tmin[b]), 0.f), hi = fmaxf(key2f(tmax[b]), 0.f);
+  float am = fmaxf(fabsf(lo), fabsf(hi));
+  gs[b] = bfr(bfr(1.0f / am) * 2688.0f);
+}
+
+__device__ __forceinline__ void store_qparams(const GP& g, int64_t gi, int scale_bytes, void* s_out, int8_t* zp_out) {
+  if (scale_bytes == 2) reinterpret_cast<uint16_t*>(s_out)[gi] = (uint16_t)g.sbits;
+  else reinterpret_cast<uint8_t*>(s_out)[gi] = (uint8_t)g.sbits;
+  if (zp_out) zp_out[gi] = (int8_t)g.zp;
+}
+
+__global__ void k_qparams_keys(QP p, const uint32_t* kmin, const uint32_t* kmax, int64_t ng,
+                               int64_t ng_item, const float* gscale, int scale_bytes, void* s_out,
+                               int8_t* zp_out) {
+  int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= ng) return;
+  float gs = (p.kind == K_NV) ? gscale[gi / ng_item] : 0.f;
+  GP g = group_params(p, key2f(kmin[gi]), key2f(kmax[gi]), gs);
+  store_qparams(g, gi, scale_bytes, s_out, zp_out);
+}
+
+__global__ void k_qparams_bf16(QP p, const uint16_t* mn, const uint16_t* mx, int64_t n,
+                               const float* gscale, int scale_bytes, void* s_out, int8_t* zp_out) {
+  int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gi >= n) return;
+  float gs = (p.kind == K_NV) ? gscale[0] : 0.f;
+  GP g = group_params(p, bf2f(mn[gi]), bf2f(mx[gi]), gs);
+  store_qparams(g, gi, scale_bytes, s_out, zp_out);
+}
+
+__global__ void k_keys_to_bf16(const uint32_t* kmin, const uint32_t* kmax, int64_t n, uint16_t* mn, uint16_t* mx) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  mn[i] = f2bf(key2f(kmin[i]));
+  mx[i] = f2bf(key2f(kmax[i]));
+}
+
+// one thread per output item (packed word / fp4 byte / element)
+__global__ void k_quant_generic(GenArgs A, QP p, int out_fmt, int scale_fmt, const void* scale,
+                                const int8_t* zp, const float* gscale, void* q_out, int64_t items_per_row,
+                                int64_t elems_per_item) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = A.batch * A.rows * items_per_row;
+  if (idx >= total) return;
+  const int64_t brow = idx / items_per_row, it = idx % items_per_row;
+  const int64_t b = brow / A.rows, r = brow % A.rows;
+  const float gs = (p.kind == K_NV) ? gscale[b] : 0.f;
+  uint32_t word = 0;
+  for (int64_t i = 0; i < elems_per_item; ++i) {
+    const int64_t c = it * elems_per_item + i;
+    if (c >= A.cols) break;
+    const int64_t gi = b * A.ng_item + group_of(A, r, c);
+    const GP g = gp_from_stored(p, scale_fmt, scale, gi, zp, gs);
+    const float x = load_w(A, b, r, c);
+    const uint32_t code = encode(p, g, x);
+    const int64_t e = brow * A.cols + c;  // dense element index
+    if (out_fmt == QZ_OUT_FAKEQUANT) {
+      float d = (p.kind == K_INT) ? fakequant_int(p, g, x) : decode(p, g, code);
+      if (A.col_scales) d = bfr(d / A.col_scales[c]);
+      reinterpret_cast<uint16_t*>(q_out)[e] = f2bf(d);
+    } else if (out_fmt == QZ_OUT_INT8) {
+      reinterpret_cast<int8_t*>(q_out)[e] = (int8_t)((int)code + (int)p.qmin);
+    } else if (out_fmt == QZ_OUT_FP8) {
+      reinterpret_cast<uint8_t*>(q_out)[e] = (uint8_t)code;
+    } else if (out_fmt == QZ_OUT_FP4_PACKED) {
+      word |= code << (4 * i);
+    } else {  // PACKED_INT32
+      word |= code << (p.bits * i);
+    }
+  }
+  if (out_fmt == QZ_OUT_PACKED_INT32) reinterpret_cast<uint32_t*>(q_out)[idx] = word;
+  else if (out_fmt == QZ_OUT_FP4_PACKED) reinterpret_cast<uint8_t*>(q_out)[idx] = (uint8_t)word;
+}
+
+__global__ void k_dequant_generic(const void* q, int64_t batch, int64_t rows, int64_t cols, QP p, int in_fmt,
+                                  GenArgs A, int scale_fmt, const void* scale, const int8_t* zp,
+                                  const float* gscale, uint16_t* out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= batch * rows * cols) return;
+  const int64_t brow = e / cols, c = e % cols;
+  const int64_t b = brow / rows, r = brow % rows;
+  uint32_t code;
+  if (in_fmt == QZ_OUT_PACKED_INT32) {
+    const int pf = 32 / p.bits;
+    const int64_t wpr = (cols + pf - 1) / pf;
+    const uint32_t word = reinterpret_cast<const uint32_t*>(q)[brow * wpr + c / pf];
+    code = (word >> (p.bits * (c % pf))) & ((1u << p.bits) - 1u);
+  } else if (in_fmt == QZ_OUT_INT8) {
+    code = (uint32_t)((int)reinterpret_cast<const int8_t*>(q)[e] - (int)p.qmin);
+  } else if (in_fmt == QZ_OUT_FP8) {
+    code = reinterpret_cast<const uint8_t*>(q)[e];
+  } else {
+    const uint8_t byte = reinterpret_cast<const uint8_t*>(q)[e >> 1];
+    code = (e & 1) ? (byte >> 4) : (byte & 15u);
+  }
+  const float gs = (p.kind == K_NV) ? gscale[b] : 0.f;
+  const int64_t gi = b * A.ng_item + group_of(A, r, c);
+  const GP g = gp_from_stored(p, scale_fmt, scale, gi, zp, gs);
+  out[e] = f2bf(decode(p, g, code));
+}
+
+__global__ void k_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int bits, int packed_dim, int32_t* out) {
+  const int pf = 32 / bits;
+  const uint32_t mask = (1u << bits) - 1u;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (packed_dim == 1) {
+    const int64_t wpr = (cols + pf - 1) / pf;
+    if (idx >= rows * wpr) return;
+    const int64_t r = idx / wpr, j = idx % wpr;
+    uint32_t word = 0;
+    for (int i = 0; i < pf; ++i) {
+      const int64_t c = j * pf + i;
+      if (c < cols) word |= ((uint32_t)(v[r * cols + c] + (1 << (bits - 1))) & mask) << (bits * i);
+    }
+    out[idx] = (int32_t)word;
+  } else {
+    const int64_t h = (rows + pf - 1) / pf;
+    if (idx >= h * cols) return;
+    const int64_t j = idx / cols, c = idx % cols;
+    uint32_t word = 0;
+    for (int i = 0; i < pf; ++i) {
+      const int64_t r = j * pf + i;
+      if (r < rows) word |= ((uint32_t)(v[r * cols + c] + (1 << (bits - 1))) & mask) << (bits * i);
+    }
+    out[idx] = (int32_t)word;
+  }
+}
+
+// ---------------------------------------------------------------------- host side
+using FastFn = void (*)(FastArgs);
+
+template <int LOGL, int KIND>
+FastFn pick_fq(bool fq) {
+  return fq ? (FastFn)k_group_fast<LOGL, KIND, true> : (FastFn)k_group_fast<LOGL, KIND, false>;
+}
+template <int LOGL>
+FastFn pick_kind(int kind, bool fq) {
+  switch (kind) {
+    case K_INT: return pick_fq<LOGL, K_INT>(fq);
+    case K_FP8: return pick_fq<LOGL, K_FP8>(fq);
+    case K_MX: return pick_fq<LOGL, K_MX>(fq);
+    case K_NV: return pick_fq<LOGL, K_NV>(fq);
+    default: return pick_fq<LOGL, K_FP4>(fq);
+  }
+}
+FastFn pick_fast(int logl, int kind, bool fq) {
+  switch (logl) {
+    case 0: return pick_kind<0>(kind, fq);
+    case 1: return pick_kind<1>(kind, fq);
+    case 2: return pick_kind<2>(kind, fq);
+    case 3: return pick_kind<3>(kind, fq);
+    case 4: return pick_kind<4>(kind, fq);
+    case 5: return pick_kind<5>(kind, fq);
+    default: return pick_kind<6>(kind, fq);
+  }
+}
+
+struct Plan {
+  QP p;
+  int kind;
+  int scale_fmt;
+  int scale_bytes;
+  int64_t ng_item;  // groups per batch item
+};
+
+int make_plan(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
+  if (!a) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0) return QZ_ERR_SHAPE;
+  QP& p = pl->p;
+  p.sym = a->symmetric ? 1 : 0;
+  p.bits = a->num_bits;
+  if (a->type == QZ_INT) {
+    if (a->num_bits < 2 || a->num_bits > 8) return QZ_ERR_BITS;
+    if (a->scale_fmt != QZ_SCALE_NATIVE) return QZ_ERR_FORMAT;
+    p.qmin = -(float)(1 << (a->num_bits - 1));
+    p.qmax = (float)((1 << (a->num_bits - 1)) - 1);
+    pl->kind = K_INT;
+  } else if (a->type == QZ_FLOAT) {
+    if (!a->symmetric) return QZ_ERR_ASYM_FLOAT;
+    if (a->num_bits == 8) {
+      if (a->scale_fmt != QZ_SCALE_NATIVE) return QZ_ERR_FORMAT;
+      p.qmin = -448.f; p.qmax = 448.f; pl->kind = K_FP8;
+    } else if (a->num_bits == 4) {
+      p.qmin = -6.f; p.qmax = 6.f;
+      if (a->scale_fmt == QZ_SCALE_E8M0) pl->kind = K_MX;
+      else if (a->strategy == QZ_TENSOR_GROUP) {
+        if (a->scale_fmt != QZ_SCALE_E4M3) return QZ_ERR_FORMAT;
+        pl->kind = K_NV;
+      } else if (a->scale_fmt == QZ_SCALE_NATIVE) pl->kind = K_FP4;
+      else return QZ_ERR_FORMAT;
+    } else return QZ_ERR_BITS;
+  } else return QZ_ERR_FORMAT;
+  p.kind = pl->kind;
+  p.half_range = (p.qmax - p.qmin) / 2.0f;
+  p.range = p.qmax - p.qmin;
+  p.magic = 8388608.0f - p.qmin;
+  pl->scale_fmt = a->scale_fmt;
+  pl->scale_bytes = (a->scale_fmt == QZ_SCALE_NATIVE) ? 2 : 1;
+  switch (a->strategy) {
+    case QZ_TENSOR: pl->ng_item = 1; break;
+    case QZ_CHANNEL: pl->ng_item = rows; break;
+    case QZ_GROUP:
+    case QZ_TENSOR_GROUP:
+      if (a->group_size <= 0 || cols % a->group_size) return QZ_ERR_GROUP;
+      if (pl->kind == K_MX && a->strategy != QZ_GROUP) return QZ_ERR_FORMAT;
+      pl->ng_item = rows * (cols / a->group_size);
+      break;
+    case QZ_BLOCK:
+      if (a->block_h <= 0 || a->block_w <= 0 || rows % a->block_h || cols % a->block_w) return QZ_ERR_BLOCK;
+      pl->ng_item = (rows / a->block_h) * (cols / a->block_w);
+      break;
+    default: return QZ_ERR_FORMAT;
+  }
+  if (pl->kind == K_NV && a->strategy != QZ_TENSOR_GROUP) return QZ_ERR_FORMAT;
+  return QZ_OK;
+}
+
+int check_out_fmt(const Plan& pl, int out_fmt) {
+  switch (out_fmt) {
+    case QZ_OUT_PACKED_INT32: return pl.kind == K_INT ? QZ_OK : QZ_ERR_FORMAT;
+    case QZ_OUT_INT8: return pl.kind == K_INT ? QZ_OK : QZ_ERR_FORMAT;
+    case QZ_OUT_FP8: return pl.kind == K_FP8 ? QZ_OK : QZ_ERR_FORMAT;
+    case QZ_OUT_FP4_PACKED: return (pl.kind == K_MX || pl.kind == K_NV || pl.kind == K_FP4) ? QZ_OK : QZ_ERR_FORMAT;
+    case QZ_OUT_FAKEQUANT: return QZ_OK;
+  }
+  return QZ_ERR_FORMAT;
+}
+
+GenArgs gen_args(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
+                 const qz_args* a, const Plan& pl, const float* col_scales) {
+  GenArgs G;
+  G.w = (const uint16_t*)w;
+  G.batch = batch; G.rows = rows; G.cols = cols; G.ld_row = ld_row; G.ld_batch = ld_batch;
+  G.strategy = a->strategy;
+  G.g = a->group_size > 0 ? a->group_size : cols;
+  G.bh = a->block_h; G.bw = a->block_w;
+  G.ng_item = pl.ng_item;
+  G.col_scales = col_scales;
+  return G;
+}
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline bool aligned(const void* p, size_t n) { return ((uintptr_t)p % n) == 0; }
+
+int launch_err() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? QZ_OK : (int)e;
+}
+
+// reduce per-group (or per-tensor) min/max keys into ws: kmin[ng], kmax[ng]
+int run_minmax(const GenArgs& G, int64_t ng_total, uint32_t* kmin, uint32_t* kmax, hipStream_t st) {
+  const int64_t nb = cdiv(ng_total, 256);
+  hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)nb), dim3(256), 0, st, kmin, ng_total, 0xffffffffu);
+  hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)nb), dim3(256), 0, st, kmax, ng_total, 0u);
+  dim3 grid((unsigned)ng_total, 1);
+  if (G.strategy == QZ_TENSOR) {
+    const int64_t elems = G.rows * G.cols;
+    grid.y = (unsigned)std::min<int64_t>(std::max<int64_t>(1, elems / (BLOCK * 64)), std::min<int64_t>(G.rows, 4096));
+  }
+  hipLaunchKernelGGL(k_minmax_generic, grid, dim3(BLOCK), 0, st, G, kmin, kmax);
+  return launch_err();
+}
+
+// workspace layout (all regions 256-B aligned):
+//   kmin[ng] u32 | kmax[ng] u32 | tmin[batch] u32 | tmax[batch] u32 |
+//   scale[ng] (2 B) | zp[ng] (1 B) | gscale[batch] f32
+struct WS {
+  uint32_t *kmin, *kmax, *tmin, *tmax;
+  void* scale;
+  int8_t* zp;
+  float* gscale;
+  size_t bytes;
+};
+inline size_t al256(size_t n) { return (n + 255) & ~(size_t)255; }
+WS ws_layout(void* base, int64_t batch, const Plan& pl) {
+  const size_t ng = (size_t)(batch * pl.ng_item);
+  WS w;
+  char* p = (char*)base;
+  size_t off = 0;
+  w.kmin = (uint32_t*)(p + off); off += al256(4 * ng);
+  w.kmax = (uint32_t*)(p + off); off += al256(4 * ng);
+  w.tmin = (uint32_t*)(p + off); off += al256(4 * (size_t)batch);
+  w.tmax = (uint32_t*)(p + off); off += al256(4 * (size_t)batch);
+  w.scale = (void*)(p + off); off += al256(2 * ng);
+  w.zp = (int8_t*)(p + off); off += al256(ng);
+  w.gscale = (float*)(p + off); off += al256(4 * (size_t)batch);
+  w.bytes = off;
+  return w;
+}
+size_t ws_size(int64_t batch, const Plan& pl) { return ws_layout(nullptr, batch, pl).bytes; }
+
+}  // namespace
+
+extern "C" {
+
+const char* qz_strerror(int code) {
+  switch (code) {
+    case QZ_OK: return "ok";
+    case QZ_ERR_NULL: return "required pointer is NULL";
+    case QZ_ERR_SHAPE: return "invalid shape";
+    case QZ_ERR_GROUP: return "tensor column shape must be divisible by the given group_size";
+    case QZ_ERR_BLOCK: return "Block quantization requires exact division";
+    case QZ_ERR_BITS: return "num_bits not supported for this type / format";
+    case QZ_ERR_ASYM_FLOAT: return "Asymmetric Quantization is not supported for float types";
+    case QZ_ERR_FORMAT: return "output/scale format incompatible with the quantization args";
+    case QZ_ERR_WORKSPACE: return "workspace too small";
+    case QZ_ERR_ALIGN: return "alignment requirement violated";
+  }
+  return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
+}
+
+int qz_version(void) { return 100; }
+
+size_t qz_quantize_workspace_size(int64_t batch, int64_t rows, int64_t cols, const qz_args* a) {
+  Plan pl;
+  if (make_plan(a, rows, cols, &pl) != QZ_OK) return 0;
+  return ws_size(batch, pl);
+}
+
+static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
+                         int64_t ld_batch, const qz_args* a, int32_t out_fmt, void* q_out, void* scale_out,
+                         int8_t* zp_out, float* gscale_out, const float* col_scales, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  if (!w || !q_out || !a) return QZ_ERR_NULL;
+  if (batch <= 0) return QZ_ERR_SHAPE;
+  Plan pl;
+  int rc = make_plan(a, rows, cols, &pl);
+  if (rc) return rc;
+  if ((rc = check_out_fmt(pl, out_fmt))) return rc;
+  if (out_fmt != QZ_OUT_FAKEQUANT && !scale_out) return QZ_ERR_NULL;
+  if (out_fmt != QZ_OUT_FAKEQUANT && pl.kind == K_NV && !gscale_out) return QZ_ERR_NULL;
+  if (ld_row < cols || (batch > 1 && ld_batch < rows * ld_row)) return QZ_ERR_SHAPE;
+  const bool fq = out_fmt == QZ_OUT_FAKEQUANT;
+  const int64_t ng = batch * pl.ng_item;
+  if (!ws || ws_bytes < ws_size(batch, pl)) return QZ_ERR_WORKSPACE;
+  const WS W = ws_layout(ws, batch, pl);
+  const bool contig = ld_row == cols && (batch == 1 || ld_batch == rows * cols);
+  if (fq && q_out == w && !contig) return QZ_ERR_FORMAT;  // in place only when dense
+  // fake-quant keeps its qparams in the workspace
+  void* s_dst = scale_out ? scale_out : W.scale;
+  int8_t* z_dst = scale_out ? zp_out : W.zp;
+  if (!pl.p.sym && !z_dst) z_dst = W.zp;
+  float* gs_dst = gscale_out ? gscale_out : W.gscale;
+
+  GenArgs G = gen_args(w, batch, rows, cols, ld_row, ld_batch, a, pl, col_scales);
+
+  // NVFP4: per-tensor global scale first
+  if (pl.kind == K_NV) {
+    GenArgs T = G;
+    T.strategy = QZ_TENSOR;
+    T.ng_item = 1;
+    if ((rc = run_minmax(T, batch, W.tmin, W.tmax, st))) return rc;
+    hipLaunchKernelGGL(k_gscale_keys, dim3((unsigned)cdiv(batch, 64)), dim3(64), 0, st, W.tmin, W.tmax, batch, gs_dst);
+    if ((rc = launch_err())) return rc;
+  }
+
+  const int64_t g = a->group_size;
+  const bool grp = a->strategy == QZ_GROUP || a->strategy == QZ_TENSOR_GROUP;
+  const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
+  const bool pack_ok = !(pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits != 4 && a->num_bits != 8);
+  const bool al = aligned(w, 16) && aligned(q_out, fq ? 16 : 8) && (!col_scales || aligned(col_scales, 16));
+  if (grp && pow2 && contig && pack_ok && al) {
+    FastArgs F;
+    F.w = (const uint16_t*)w;
+    F.n_units = batch * rows * cols / 8;
+    F.units_per_batch = rows * cols / 8;
+    F.units_per_row = cols / 8;
+    F.p = pl.p;
+    F.out_fmt = out_fmt;
+    F.scale_bytes = pl.scale_bytes;
+    F.q_out = q_out;
+    F.s_out = s_dst;
+    F.zp_out = z_dst;
+    F.gscale = gs_dst;
+    F.col_scales = col_scales;
+    int logl = 0;
+    while ((8 << logl) < g) ++logl;
+    const int64_t waves = cdiv(F.n_units, UNROLL * WAVE);
+    const int64_t blocks = cdiv(waves, BLOCK / WAVE);
+    hipLaunchKernelGGL(pick_fast(logl, pl.kind, fq), dim3((unsigned)blocks), dim3(BLOCK), 0, st, F);
+    return launch_err();
+  }
+
+  // generic: min/max -> qparams -> quantize
+  if ((rc = run_minmax(G, ng, W.kmin, W.kmax, st))) return rc;
+  hipLaunchKernelGGL(k_qparams_keys, dim3((unsigned)cdiv(ng, 256)), dim3(256), 0, st, pl.p, W.kmin, W.kmax, ng,
+                     pl.ng_item, (const float*)gs_dst, pl.scale_bytes, s_dst, z_dst);
+  if ((rc = launch_err())) return rc;
+  int64_t per_item = 1;
+  if (out_fmt == QZ_OUT_PACKED_INT32) per_item = 32 / a->num_bits;
+  else if (out_fmt == QZ_OUT_FP4_PACKED) per_item = 2;
+  const int64_t ipr = cdiv(cols, per_item);
+  const int64_t items = batch * rows * ipr;
+  hipLaunchKernelGGL(k_quant_generic, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, G, pl.p, (int)out_fmt,
+                     pl.scale_fmt, (const void*)s_dst, (const int8_t*)z_dst, (const float*)gs_dst, q_out, ipr,
+                     per_item);
+  return launch_err();
+}
+
+int qz_quantize(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
+                const qz_args* a, int32_t out_fmt, void* q_out, void* scale_out, int8_t* zp_out, float* gscale_out,
+                void* workspace, size_t workspace_bytes, qz_stream_t stream) {
+  return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, out_fmt, q_out, scale_out, zp_out, gscale_out,
+                       nullptr, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
+                      const qz_args* a, const float* col_scales, void* w_out, void* workspace, size_t workspace_bytes,
+                      qz_stream_t stream) {
+  return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, QZ_OUT_FAKEQUANT, w_out, nullptr, nullptr, nullptr,
+                       col_scales, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qz_quantize_qparams(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
+                        const qz_args* a, int32_t out_fmt, const void* scale, const int8_t* zp, const float* gscale,
+                        void* q_out, qz_stream_t stream) {
+  if (!w || !q_out || !scale || !a) return QZ_ERR_NULL;
+  if (batch <= 0) return QZ_ERR_SHAPE;
+  Plan pl;
+  int rc = make_plan(a, rows, cols, &pl);
+  if (rc) return rc;
+  if ((rc = check_out_fmt(pl, out_fmt))) return rc;
+  if (pl.kind == K_NV && !gscale) return QZ_ERR_NULL;
+  if (!pl.p.sym && !zp) return QZ_ERR_NULL;
+  if (ld_row < cols || (batch > 1 && ld_batch < rows * ld_row)) return QZ_ERR_SHAPE;
+  GenArgs G = gen_args(w, batch, rows, cols, ld_row, ld_batch, a, pl, nullptr);
+  int64_t per_item = 1;
+  if (out_fmt == QZ_OUT_PACKED_INT32) per_item = 32 / a->num_bits;
+  else if (out_fmt == QZ_OUT_FP4_PACKED) per_item = 2;
+  const int64_t ipr = cdiv(cols, per_item);
+  const int64_t items = batch * rows * ipr;
+  hipLaunchKernelGGL(k_quant_generic, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, (hipStream_t)stream, G, pl.p,
+                     (int)out_fmt, pl.scale_fmt, scale, zp, gscale, q_out, ipr, per_item);
+  return launch_err();
+}
+
+int qz_observe_minmax(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
+                      const qz_args* a, void* min_out, void* max_out, void* workspace, size_t workspace_bytes,
+                      qz_stream_t stream) {
+  if (!w || !min_out || !max_out || !a) return QZ_ERR_NULL;
+  Plan pl;
+  qz_args a2 = *a;
+  if (a2.strategy == QZ_TENSOR_GROUP) a2.strategy = QZ_GROUP;
+  int rc = make_plan(&a2, rows, cols, &pl);
+  if (rc == QZ_ERR_FORMAT) rc = QZ_OK;  // observation does not depend on the format
+  if (rc) return rc;
+  if (a2.strategy == QZ_TENSOR) pl.ng_item = 1;
+  else if (a2.strategy == QZ_CHANNEL) pl.ng_item = rows;
+  else if (a2.strategy == QZ_BLOCK) pl.ng_item = (rows / a2.block_h) * (cols / a2.block_w);
+  else pl.ng_item = rows * (cols / a2.group_size);
+  const int64_t ng = batch * pl.ng_item;
+  if (!workspace || workspace_bytes < (size_t)8 * ng) return QZ_ERR_WORKSPACE;
+  uint32_t* kmin = (uint32_t*)workspace;
+  uint32_t* kmax = kmin + ng;
+  GenArgs G = gen_args(w, batch, rows, cols, ld_row, ld_batch, &a2, pl, nullptr);
+  if ((rc = run_minmax(G, ng, kmin, kmax, (hipStream_t)stream))) return rc;
+  hipLaunchKernelGGL(k_keys_to_bf16, dim3((unsigned)cdiv(ng, 256)), dim3(256), 0, (hipStream_t)stream, kmin, kmax, ng,
+                     (uint16_t*)min_out, (uint16_t*)max_out);
+  return launch_err();
+}
+
+int qz_calculate_qparams(const void* min_vals, const void* max_vals, int64_t n, const qz_args* a,
+                         const float* gscale, void* scale_out, int8_t* zp_out, qz_stream_t stream) {
+  if (!min_vals || !max_vals || !scale_out || !a) return QZ_ERR_NULL;
+  if (n <= 0) return QZ_ERR_SHAPE;
+  Plan pl;
+  qz_args a2 = *a;
+  int rc = make_plan(&a2, 1, a2.group_size > 0 ? a2.group_size : 1, &pl);
+  if (rc == QZ_ERR_BLOCK || rc == QZ_ERR_GROUP) rc = QZ_OK;
+  if (rc) return rc;
+  if (pl.kind == K_NV && !gscale) return QZ_ERR_NULL;
+  hipLaunchKernelGGL(k_qparams_bf16, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, pl.p,
+                     (const uint16_t*)min_vals, (const uint16_t*)max_vals, n, gscale, pl.scale_bytes, scale_out, zp_out);
+  return launch_err();
+}
+
+int qz_dequantize(const void* q, int64_t batch, int64_t rows, int64_t cols, const qz_args* a, int32_t in_fmt,
+                  const void* scale, const int8_t* zp, const float* gscale, void* w_out, qz_stream_t stream) {
+  if (!q || !a || !scale || !w_out) return QZ_ERR_NULL;
+  if (batch <= 0) return QZ_ERR_SHAPE;
+  Plan pl;
+  int rc = make_plan(a, rows, cols, &pl);
+  if (rc) return rc;
+  if (in_fmt == QZ_OUT_FAKEQUANT || (rc = check_out_fmt(pl, in_fmt))) return rc ? rc : QZ_ERR_FORMAT;
+  if (pl.kind == K_NV && !gscale) return QZ_ERR_NULL;
+  if (!pl.p.sym && !zp) return QZ_ERR_NULL;
+  GenArgs G = gen_args(nullptr, batch, rows, cols, cols, rows * cols, a, pl, nullptr);
+  const int64_t n = batch * rows * cols;
+  hipLaunchKernelGGL(k_dequant_generic, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, q, batch,
+                     rows, cols, pl.p, (int)in_fmt, G, pl.scale_fmt, scale, zp, gscale, (uint16_t*)w_out);
+  return launch_err();
+}
+
+int qz_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int32_t num_bits, int32_t packed_dim, int32_t* out,
+                  qz_stream_t stream) {
+  if (!v || !out) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0) return QZ_ERR_SHAPE;
+  if (num_bits < 1 || num_bits > 8) return QZ_ERR_BITS;
+  if (packed_dim != 0 && packed_dim != 1) return QZ_ERR_FORMAT;
+  const int pf = 32 / num_bits;
+  const int64_t n = packed_dim == 1 ? rows * cdiv(cols, pf) : cdiv(rows, pf) * cols;
+  hipLaunchKernelGGL(k_pack_int32, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, v, rows, cols,
+                     (int)num_bits, (int)packed_dim, out);
+  return launch_err();
+}
+
+}  // extern "C"

@@ -1,0 +1,408 @@
+"""PyTorch-facing wrappers of the HIP quantization kernels (device memory + stream plumbing).
+
+Names and argument meaning follow compressed-tensors / llmcompressor (the reference's
+quantization dependencies, called from scripts/do_oneshot.py:179-197):
+
+=========================  ==========================================================
+this module                 replaces ([3P] = third-party)
+=========================  ==========================================================
+``observe_minmax``          llmcompressor observer ``memoryless_minmax`` (a7)
+``calculate_qparams``       compressed_tensors ``calculate_qparams`` (a8)
+``quantize``                compressed_tensors ``quantize`` with given qparams (a9)
+``fake_quantize``           compressed_tensors ``fake_quantize`` (AWQ grid, a5)
+``dequantize``              compressed_tensors ``dequantize`` / decompressors
+``pack_to_int32``           compressed_tensors ``pack_to_int32`` (a10)
+``compress_weight``         observer -> qparams -> quantize -> pack, one fused pass
+                            (ModelCompressor.compress_model per module, a9-a12)
+``awq_*``                   llmcompressor AWQModifier statistics / smoothing (a3-a6)
+=========================  ==========================================================
+
+All tensors must live on a ROCm device; weights are bf16 2-D ``[N, K]`` or a 3-D batch of
+slices ``[E, N, K]`` (fused MoE experts).  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+from .quantization import QuantizationArgs
+
+_P = ctypes.c_void_p
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return _P(t.data_ptr()) if t is not None else _P(0)
+
+
+def _stream():
+    return _P(torch.cuda.current_stream().cuda_stream)
+
+
+def _check_dev(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a ROCm device tensor (no CPU fallback)")
+
+
+_ws_cache: Dict[Tuple[int, int], torch.Tensor] = {}
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    """Per-(device, stream) grow-only scratch buffer (the library never allocates)."""
+    dev = torch.device(device)
+    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+        _ws_cache[key] = buf
+    return buf
+
+
+def _geom(w: torch.Tensor):
+    """(batch, rows, cols, ld_row, ld_batch) for a 2-D or 3-D bf16 weight view."""
+    if w.dtype != torch.bfloat16:
+        raise ValueError(f"weights must be bfloat16 (got {w.dtype})")
+    if w.dim() == 2:
+        w3 = w.unsqueeze(0)
+    elif w.dim() == 3:
+        w3 = w
+    else:
+        raise ValueError("weight must be 2-D [N, K] or 3-D [E, N, K]")
+    if w3.stride(2) != 1:
+        raise ValueError("weight rows must be contiguous (stride(-1) == 1)")
+    b, r, c = w3.shape
+    ld_b = w3.stride(0) if b > 1 else r * w3.stride(1)
+    return b, r, c, w3.stride(1), ld_b
+
+
+def n_groups(a: QuantizationArgs, rows: int, cols: int) -> Tuple[int, ...]:
+    """Per-slice scale shape (compressed-tensors layout)."""
+    if a.strategy == "tensor":
+        return (1,)
+    if a.strategy == "channel":
+        return (rows, 1)
+    if a.strategy in ("group", "tensor_group"):
+        if cols % a.group_size:
+            raise ValueError(f"tensor column shape must be divisible by the given group_size {a.group_size}")
+        return (rows, cols // a.group_size)
+    if a.strategy == "block":
+        bh, bw = a.block_structure
+        if rows % bh or cols % bw:
+            raise ValueError("Block quantization requires exact division")
+        return (rows // bh, cols // bw)
+    raise ValueError(f"strategy {a.strategy} not supported for weights")
+
+
+def _scale_dtype(a: QuantizationArgs):
+    if a.is_mx:
+        return torch.uint8
+    if a.is_nvfp4:
+        return torch.float8_e4m3fn
+    return torch.bfloat16
+
+
+def default_out_fmt(a: QuantizationArgs) -> int:
+    if a.type == "int":
+        return _lib.QZ_OUT_PACKED_INT32
+    if a.num_bits == 8:
+        return _lib.QZ_OUT_FP8
+    return _lib.QZ_OUT_FP4_PACKED
+
+
+def _alloc_codes(out_fmt: int, a: QuantizationArgs, lead, rows, cols, device):
+    if out_fmt == _lib.QZ_OUT_PACKED_INT32:
+        pf = 32 // a.num_bits
+        return torch.empty(*lead, rows, (cols + pf - 1) // pf, dtype=torch.int32, device=device)
+    if out_fmt == _lib.QZ_OUT_INT8:
+        return torch.empty(*lead, rows, cols, dtype=torch.int8, device=device)
+    if out_fmt == _lib.QZ_OUT_FP8:
+        return torch.empty(*lead, rows, cols, dtype=torch.float8_e4m3fn, device=device)
+    if out_fmt == _lib.QZ_OUT_FP4_PACKED:
+        return torch.empty(*lead, rows, cols // 2, dtype=torch.uint8, device=device)
+    return torch.empty(*lead, rows, cols, dtype=torch.bfloat16, device=device)
+
+
+def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int] = None,
+                    out: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+    """Fused memoryless observe + calculate_qparams + quantize (+ pack).
+
+    Returns ``codes`` (packed int32 / int8 / e4m3 / packed fp4), ``scale``, ``zero_point``
+    (int8 per group) and, for NVFP4, ``global_scale`` (f32 per slice).  ``out`` may supply
+    preallocated tensors (bench / graph capture).
+    """
+    _check_dev(w, "weight")
+    b, r, c, ld_r, ld_b = _geom(w)
+    lead = tuple(w.shape[:-2])
+    out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+    ca = a.to_c()
+    gshape = n_groups(a, r, c)
+    dev = w.device
+    o = dict(out or {})
+    if "codes" not in o:
+        o["codes"] = _alloc_codes(out_fmt, a, lead, r, c, dev)
+    if "scale" not in o:
+        o["scale"] = torch.empty(*lead, *gshape, dtype=_scale_dtype(a), device=dev)
+    if "zero_point" not in o:
+        o["zero_point"] = torch.empty(*lead, *gshape, dtype=torch.int8, device=dev)
+    if a.is_nvfp4 and "global_scale" not in o:
+        o["global_scale"] = torch.empty(max(b, 1), dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    ws_n = lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca))
+    ws = o.get("workspace")
+    if ws is None or ws.numel() < ws_n:
+        ws = workspace(ws_n, dev)
+    rc = lib.qz_quantize(_ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), out_fmt, _ptr(o["codes"]),
+                         _ptr(o["scale"]), _ptr(o["zero_point"]), _ptr(o.get("global_scale")),
+                         _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "qz_quantize")
+    o.pop("workspace", None)
+    return o
+
+
+def fake_quantize(w: torch.Tensor, a: QuantizationArgs, col_scales: Optional[torch.Tensor] = None,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``fake_quantize(w)`` with memoryless qparams; with ``col_scales`` s it is AWQ's
+    ``Q(W * s) / s`` (llmcompressor _compute_best_scale inner step), one fused pass."""
+    _check_dev(w, "weight")
+    b, r, c, ld_r, ld_b = _geom(w)
+    if out is None:
+        out = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
+    if col_scales is not None:
+        col_scales = col_scales.to(device=w.device, dtype=torch.float32).contiguous()
+        if col_scales.numel() != c:
+            raise ValueError("col_scales must have one entry per input column")
+    ca = a.to_c()
+    lib = _lib.load()
+    ws_n = lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca)) + 4 * b + 256
+    ws = workspace(ws_n, w.device)
+    rc = lib.qz_awq_fake_quant(_ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), _ptr(col_scales), _ptr(out),
+                               _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "qz_awq_fake_quant")
+    return out
+
+
+def observe_minmax(w: torch.Tensor, a: QuantizationArgs) -> Tuple[torch.Tensor, torch.Tensor]:
+    _check_dev(w, "weight")
+    b, r, c, ld_r, ld_b = _geom(w)
+    lead = tuple(w.shape[:-2])
+    a2 = a if a.strategy != "tensor_group" else QuantizationArgs(
+        num_bits=a.num_bits, type=a.type, symmetric=a.symmetric, strategy="group", group_size=a.group_size)
+    gshape = n_groups(a2, r, c)
+    mn = torch.empty(*lead, *gshape, dtype=torch.bfloat16, device=w.device)
+    mx = torch.empty_like(mn)
+    ng = mn.numel()
+    ws = workspace(8 * ng + 256, w.device)
+    ca = a.to_c()
+    rc = _lib.load().qz_observe_minmax(_ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), _ptr(mn), _ptr(mx),
+                                       _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "qz_observe_minmax")
+    return mn, mx
+
+
+def calculate_qparams(min_vals: torch.Tensor, max_vals: torch.Tensor, a: QuantizationArgs,
+                      global_scale: Optional[torch.Tensor] = None):
+    """compressed-tensors ``calculate_qparams`` on device (bf16 min/max in, scale/zp out)."""
+    _check_dev(min_vals, "min_vals")
+    mn = min_vals.to(torch.bfloat16).contiguous()
+    mx = max_vals.to(torch.bfloat16).contiguous()
+    scale = torch.empty(mn.shape, dtype=_scale_dtype(a), device=mn.device)
+    zp = torch.empty(mn.shape, dtype=torch.int8, device=mn.device)
+    gs = None
+    if a.is_nvfp4:
+        if global_scale is None:
+            raise ValueError("NVFP4 qparams need a global_scale")
+        gs = global_scale.to(torch.float32).contiguous()
+    ca = a.to_c()
+    rc = _lib.load().qz_calculate_qparams(_ptr(mn), _ptr(mx), mn.numel(), ctypes.byref(ca), _ptr(gs),
+                                          _ptr(scale), _ptr(zp), _stream())
+    _lib.check(rc, "qz_calculate_qparams")
+    return scale, zp
+
+
+def quantize(w: torch.Tensor, scale: torch.Tensor, zero_point: Optional[torch.Tensor], a: QuantizationArgs,
+             out_fmt: Optional[int] = None, global_scale: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """compressed-tensors ``quantize`` with caller-supplied qparams -> codes in ``out_fmt``."""
+    _check_dev(w, "weight")
+    b, r, c, ld_r, ld_b = _geom(w)
+    lead = tuple(w.shape[:-2])
+    out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+    codes = _alloc_codes(out_fmt, a, lead, r, c, w.device)
+    ca = a.to_c()
+    zp = zero_point.to(torch.int8).contiguous() if zero_point is not None else None
+    gs = global_scale.to(torch.float32).contiguous() if global_scale is not None else None
+    rc = _lib.load().qz_quantize_qparams(_ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), out_fmt,
+                                         _ptr(scale.contiguous()), _ptr(zp), _ptr(gs), _ptr(codes), _stream())
+    _lib.check(rc, "qz_quantize_qparams")
+    return codes
+
+
+def dequantize(codes: torch.Tensor, shape, a: QuantizationArgs, scale: torch.Tensor,
+               zero_point: Optional[torch.Tensor] = None, global_scale: Optional[torch.Tensor] = None,
+               in_fmt: Optional[int] = None) -> torch.Tensor:
+    """Decompress codes back to bf16 ``shape`` ([N, K] or [E, N, K])."""
+    _check_dev(codes, "codes")
+    in_fmt = default_out_fmt(a) if in_fmt is None else in_fmt
+    shape = tuple(int(s) for s in shape)
+    if len(shape) == 2:
+        b, (r, c) = 1, shape
+    else:
+        b, r, c = shape
+    out = torch.empty(shape, dtype=torch.bfloat16, device=codes.device)
+    zp = zero_point.to(torch.int8).contiguous() if zero_point is not None else None
+    gs = global_scale.to(torch.float32).contiguous() if global_scale is not None else None
+    ca = a.to_c()
+    rc = _lib.load().qz_dequantize(_ptr(codes.contiguous()), b, r, c, ctypes.byref(ca), in_fmt,
+                                   _ptr(scale.contiguous()), _ptr(zp), _ptr(gs), _ptr(out), _stream())
+    _lib.check(rc, "qz_dequantize")
+    return out
+
+
+def pack_to_int32(value: torch.Tensor, num_bits: int, packed_dim: int = 1) -> torch.Tensor:
+    """compressed-tensors ``pack_to_int32`` (int8 [R, C] -> int32)."""
+    _check_dev(value, "value")
+    if value.dtype != torch.int8:
+        raise ValueError("Tensor must be quantized to torch.int8 before packing")
+    if num_bits > 8:
+        raise ValueError("Packing is only supported for less than 8 bits")
+    v = value.contiguous()
+    r, c = v.shape
+    pf = 32 // num_bits
+    shape = (r, (c + pf - 1) // pf) if packed_dim == 1 else ((r + pf - 1) // pf, c)
+    out = torch.empty(shape, dtype=torch.int32, device=v.device)
+    rc = _lib.load().qz_pack_int32(_ptr(v), r, c, num_bits, packed_dim, _ptr(out), _stream())
+    _lib.check(rc, "qz_pack_int32")
+    return out
+
+
+def compress_weight(w: torch.Tensor, a: QuantizationArgs, has_activation_quant: bool = False) -> Dict[str, torch.Tensor]:
+    """One module's on-disk tensors (names pinned by scripts/recombine_weights_MiniMax-M2.1.py:54-65):
+    pack-quantized -> weight_packed/weight_scale/weight_shape[/weight_zero_point];
+    float-quantized -> weight/weight_scale; nvfp4/mxfp4-pack-quantized -> weight_packed/weight_scale
+    [/weight_global_scale]."""
+    out: Dict[str, torch.Tensor] = {}
+    if a.type == "int":
+        int_q = has_activation_quant and a.num_bits == 8
+        fmt = _lib.QZ_OUT_INT8 if (int_q or a.num_bits not in (4, 8)) else _lib.QZ_OUT_PACKED_INT32
+        q = quantize_weight(w, a, out_fmt=fmt)
+        codes = q["codes"]
+        if fmt == _lib.QZ_OUT_INT8 and not int_q:
+            codes = pack_to_int32(codes.reshape(-1, codes.shape[-1]), a.num_bits).reshape(
+                *codes.shape[:-1], -1)
+        if int_q:
+            out["weight"] = codes
+        else:
+            out["weight_packed"] = codes
+            out["weight_shape"] = torch.tensor(list(w.shape[-2:]))
+        out["weight_scale"] = q["scale"]
+        if not a.symmetric and a.strategy in ("group", "channel"):
+            zp = q["zero_point"]
+            if int_q:
+                out["weight_zero_point"] = zp
+            else:
+                if zp.dim() == 2:
+                    out["weight_zero_point"] = pack_to_int32(zp, a.num_bits, packed_dim=0)
+                else:
+                    out["weight_zero_point"] = torch.stack([pack_to_int32(z, a.num_bits, packed_dim=0) for z in zp])
+        return out
+    q = quantize_weight(w, a)
+    if a.num_bits == 8:
+        out["weight"] = q["codes"]
+        out["weight_scale"] = q["scale"]
+    else:
+        out["weight_packed"] = q["codes"]
+        out["weight_scale"] = q["scale"]
+        if a.is_nvfp4:
+            gs = q["global_scale"]
+            out["weight_global_scale"] = gs if w.dim() == 3 else gs.reshape(1)
+    return out
+
+
+# ------------------------------------------------------------------------------- AWQ
+def awq_absmean_accum(x: torch.Tensor, sums: torch.Tensor) -> int:
+    """sums[c] += sum_t |x[t, c]| (fp32, deterministic).  Returns the token count added."""
+    _check_dev(x, "activations")
+    if x.dtype != torch.bfloat16:
+        x = x.to(torch.bfloat16)
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    t, c = x2.shape
+    lib = _lib.load()
+    ws = workspace(lib.qz_awq_absmean_workspace_size(t, c) + 256, x.device)
+    rc = lib.qz_awq_absmean_accum(_ptr(x2), t, c, x2.stride(0), _ptr(sums), _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "qz_awq_absmean_accum")
+    return t
+
+
+def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) -> int:
+    """wsum[c] += sum_r |W[r,c]| / (group absmax + 1e-6) (fp64).  Returns rows added."""
+    _check_dev(w, "weight")
+    w2 = w.reshape(-1, w.shape[-1])
+    if w2.stride(-1) != 1:
+        w2 = w2.contiguous()
+    r, c = w2.shape
+    rc = _lib.load().qz_awq_weight_mean_accum(_ptr(w2), r, c, w2.stride(0), int(group_size), _ptr(wsum), _stream())
+    _lib.check(rc, "qz_awq_weight_mean_accum")
+    return r
+
+
+def awq_grid_scales(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo_scaling: bool,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    x_mean = x_mean.to(torch.float32).contiguous()
+    wm = w_mean.to(torch.float32).contiguous() if w_mean is not None else None
+    if out is None:
+        out = torch.empty_like(x_mean)
+    rc = _lib.load().qz_awq_grid_scales(_ptr(x_mean), _ptr(wm), x_mean.numel(), float(ratio), int(duo_scaling),
+                                        _ptr(out), _stream())
+    _lib.check(rc, "qz_awq_grid_scales")
+    return out
+
+
+def scale_columns_(w: torch.Tensor, s: torch.Tensor, divide: bool = False) -> torch.Tensor:
+    """In place W[:, c] *= s[c] (or /=), bf16-rounded (AWQ _apply_smoothing, balance layers)."""
+    _check_dev(w, "weight")
+    w2 = w.reshape(-1, w.shape[-1]) if w.dim() != 1 else w.reshape(1, -1)
+    s = s.to(device=w.device, dtype=torch.float32).contiguous()
+    rc = _lib.load().qz_scale_columns(_ptr(w2), w2.shape[0], w2.shape[1], w2.stride(0), _ptr(s), int(divide),
+                                      _stream())
+    _lib.check(rc, "qz_scale_columns")
+    return w
+
+
+def scale_rows_(w: torch.Tensor, s: torch.Tensor, divide: bool = True) -> torch.Tensor:
+    """In place W[r, :] /= s[r] (or *=): smooth Linear's output rows, 1-D norm weights, biases."""
+    _check_dev(w, "weight")
+    w2 = w.reshape(-1, 1) if w.dim() == 1 else w
+    s = s.to(device=w.device, dtype=torch.float32).contiguous()
+    rc = _lib.load().qz_scale_rows(_ptr(w2), w2.shape[0], w2.shape[1], w2.stride(0), _ptr(s), int(divide),
+                                   _stream())
+    _lib.check(rc, "qz_scale_rows")
+    return w
+
+
+class PreparedQuantize:
+    """A qz_quantize call with every argument marshalled once (bench / tight host loops):
+    ``run(w)`` costs one ctypes call + one kernel launch.  Graph-capturable."""
+
+    def __init__(self, w_like: torch.Tensor, a: QuantizationArgs, out: Dict[str, torch.Tensor],
+                 out_fmt: Optional[int] = None):
+        self.geom = _geom(w_like)
+        b, r, c, _, _ = self.geom
+        self.ca = a.to_c()
+        self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+        self.lib = _lib.load()
+        n = self.lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(self.ca))
+        self.ws = torch.empty(max(n, 256), dtype=torch.uint8, device=w_like.device)
+        self.out = out
+        self._args_tail = (ctypes.byref(self.ca), self.out_fmt, _ptr(out["codes"]), _ptr(out["scale"]),
+                           _ptr(out.get("zero_point")), _ptr(out.get("global_scale")), _ptr(self.ws),
+                           self.ws.numel())
+
+    def run(self, w: torch.Tensor, stream=None) -> None:
+        b, r, c, ld_r, ld_b = self.geom
+        st = _P(stream.cuda_stream) if stream is not None else _stream()
+        rc = self.lib.qz_quantize(_P(w.data_ptr()), b, r, c, ld_r, ld_b, *self._args_tail, st)
+        if rc:
+            _lib.check(rc, "qz_quantize")

@@ -1,0 +1,34 @@
+"""The C-ABI library loads and exports every function include/quantizers_amd.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "quantizers_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(qz_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_header_symbols():
+    from quantizers_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    decl = _declared()
+    assert len(decl) >= 16
+    missing = [n for n in decl if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(decl) == set(_lib.EXPORTS)
+
+
+def test_host_only_entry_points():
+    from quantizers_amd import _lib
+    lib = _lib.load()
+    assert lib.qz_version() == 100
+    assert lib.qz_strerror(-3).decode().startswith("tensor column shape")
+    a = _lib.QzArgs(4, 0, 1, 2, 128, 0, 0, 0)
+    assert lib.qz_quantize_workspace_size(1, 11008, 4096, ctypes.byref(a)) > 0
+    bad = _lib.QzArgs(4, 0, 1, 2, 100, 0, 0, 0)
+    assert lib.qz_quantize_workspace_size(1, 16, 128, ctypes.byref(bad)) == 0

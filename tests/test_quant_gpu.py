@@ -1,0 +1,248 @@
+"""GPU parity: the HIP library (through the C ABI) vs the CPU oracle, bit for bit.
+
+Bar (BASELINE.json north_star): packed int words, integer zero-points, scales and FP8/FP4 codes
+identical to the CPU restatement (oracle/ct_torch.py, itself pinned by oracle/quant_ref.c and
+the KATs).  Every scheme the reference's recipes use, plus edge cases (all-zero groups, ties at
++-7.5*s, outliers, ragged shapes, fused-expert batches, strided views).
+"""
+import pytest
+import torch
+
+import ct_torch as ct
+from quantizers_amd import ops, _lib
+from quantizers_amd.quantization import QuantizationArgs
+
+pytestmark = pytest.mark.gpu
+
+
+def _w(n, k, seed=0, scale=0.02, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.randn(n, k, generator=g) * scale).to(torch.bfloat16)
+    return w
+
+
+def _edge_weight(n, k, g, seed=1):
+    w = _w(n, k, seed).float()
+    gen = torch.Generator().manual_seed(seed + 100)
+    m = torch.rand(n, k, generator=gen) < 0.001
+    w[m] *= 20  # outliers
+    w[0, :g] = 0  # an all-zero group
+    if n > 2 and k >= g:  # exact ties at +-7.5*s and +-0.5*s
+        w[2, :g] = 0.0
+        w[2, 0] = 0.75
+        w[2, 1] = -0.75
+        w[2, 2] = 0.05
+        w[2, 3] = -0.05
+        w[2, 4] = 0.15
+    return w.to(torch.bfloat16)
+
+
+def _oracle_args(a: QuantizationArgs) -> ct.QArgs:
+    sd = {None: None, "float8_e4m3fn": "fp8", "uint8": "e8m0"}[a.scale_dtype]
+    return ct.QArgs(num_bits=a.num_bits, type=a.type, symmetric=a.symmetric, strategy=a.strategy,
+                    group_size=a.group_size, block_structure=tuple(a.block_structure) if a.block_structure else None,
+                    scale_dtype=sd)
+
+
+def _eq(a: torch.Tensor, b: torch.Tensor):
+    a = a.cpu()
+    b = b.cpu()
+    assert a.shape == b.shape, (a.shape, b.shape)
+    if a.dtype in (torch.bfloat16, torch.float8_e4m3fn):
+        a = a.view(torch.uint8 if a.dtype == torch.float8_e4m3fn else torch.int16)
+        b = b.view(torch.uint8 if b.dtype == torch.float8_e4m3fn else torch.int16)
+    bad = (a != b)
+    assert not bad.any(), f"{int(bad.sum())} / {bad.numel()} mismatches; first at {bad.nonzero()[:5].tolist()}"
+
+
+SCHEMES = [
+    dict(num_bits=4, type="int", symmetric=True, group_size=128),
+    dict(num_bits=4, type="int", symmetric=True, group_size=32),
+    dict(num_bits=4, type="int", symmetric=True, group_size=64),
+    dict(num_bits=4, type="int", symmetric=False, group_size=128),
+    dict(num_bits=4, type="int", symmetric=False, group_size=32),
+    dict(num_bits=8, type="int", symmetric=True, group_size=128),
+    dict(num_bits=8, type="int", symmetric=False, group_size=64),
+    dict(num_bits=4, type="int", symmetric=True, strategy="channel"),
+    dict(num_bits=8, type="int", symmetric=True, strategy="channel"),
+    dict(num_bits=4, type="int", symmetric=False, strategy="channel"),
+    dict(num_bits=4, type="int", symmetric=True, strategy="tensor"),
+    dict(num_bits=8, type="float", group_size=32),
+    dict(num_bits=8, type="float", group_size=128),
+    dict(num_bits=8, type="float", strategy="channel"),
+    dict(num_bits=8, type="float", strategy="tensor"),
+    dict(num_bits=8, type="float", strategy="block", block_structure=[128, 128]),
+    dict(num_bits=8, type="float", strategy="block", block_structure=[64, 32]),
+    dict(num_bits=4, type="float", group_size=32, scale_dtype="uint8"),  # MXFP4
+    dict(num_bits=4, type="float", strategy="tensor_group", group_size=16, scale_dtype="float8_e4m3fn"),  # NVFP4
+    dict(num_bits=4, type="int", symmetric=True, group_size=256),
+    dict(num_bits=4, type="int", symmetric=True, group_size=512),
+    dict(num_bits=4, type="int", symmetric=True, group_size=16),
+]
+
+
+def _id(d):
+    return "-".join(f"{k}{v}" for k, v in d.items() if k not in ("type",)) + "-" + d["type"]
+
+
+@pytest.mark.parametrize("scheme", SCHEMES, ids=_id)
+@pytest.mark.parametrize("shape", [(256, 512), (384, 1024)])
+def test_compress_matches_oracle(cuda, scheme, shape):
+    a = QuantizationArgs(**scheme)
+    n, k = shape
+    gsz = a.group_size or (a.block_structure[1] if a.block_structure else k)
+    w = _edge_weight(n, k, max(1, min(gsz, k)))
+    ref = ct.compress_weight(w, _oracle_args(a))
+    got = ops.compress_weight(w.to(cuda), a)
+    assert set(got) == set(ref), (set(got), set(ref))
+    for key in ref:
+        _eq(got[key], ref[key])
+
+
+@pytest.mark.parametrize("scheme", SCHEMES[:8] + SCHEMES[11:19], ids=_id)
+def test_fake_quantize_matches_oracle(cuda, scheme):
+    a = QuantizationArgs(**scheme)
+    w = _edge_weight(128, 512, 32)
+    oa = _oracle_args(a)
+    gs = None
+    if oa.strategy == "tensor_group":
+        gs = ct.generate_gparam(w.amin().reshape(1), w.amax().reshape(1))
+    mn, mx = ct.observe_minmax(w, oa)
+    s, z = ct.calculate_qparams(mn, mx, oa, global_scale=gs)
+    ref = ct.fake_quantize(w, s, z, oa, global_scale=gs)
+    got = ops.fake_quantize(w.to(cuda), a)
+    _eq(got, ref)
+
+
+@pytest.mark.parametrize("scheme", [SCHEMES[0], SCHEMES[1], SCHEMES[3], SCHEMES[11], SCHEMES[17], SCHEMES[18],
+                                    SCHEMES[7]], ids=_id)
+def test_awq_fake_quant_scaled(cuda, scheme):
+    a = QuantizationArgs(**scheme)
+    w = _w(96, 512, seed=3)
+    g = torch.Generator().manual_seed(7)
+    s = (torch.rand(512, generator=g) * 3 + 0.05).float()
+    ref = ct.awq_fake_quant_scaled(w, s, _oracle_args(a))
+    got = ops.fake_quantize(w.to(cuda), a, col_scales=s.to(cuda))
+    _eq(got, ref)
+
+
+def test_headline_shape_int4_g128(cuda):
+    """The bench workload: bf16 [11008, 4096], int4 sym g128 (compared in full)."""
+    w = _w(11008, 4096, seed=0)
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    import qref
+    ref_p, ref_s = qref.int_sym_group_pack(w, 4, 128)
+    got = ops.quantize_weight(w.to(cuda), a)
+    _eq(got["codes"], ref_p)
+    _eq(got["scale"], ref_s)
+
+
+def test_batched_experts_and_strided(cuda):
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    e = torch.stack([_w(64, 256, seed=i) for i in range(5)])
+    got = ops.compress_weight(e.to(cuda), a)
+    for i in range(5):
+        ref = ct.compress_weight(e[i], _oracle_args(a))
+        _eq(got["weight_packed"][i], ref["weight_packed"])
+        _eq(got["weight_scale"][i], ref["weight_scale"])
+    # strided view (columns of a wider buffer) -> generic path, same answer
+    big = _w(64, 384, seed=9)
+    view = big.to(cuda)[:, 64:320]
+    ref = ct.compress_weight(big[:, 64:320].contiguous(), _oracle_args(a))
+    got = ops.compress_weight(view, a)
+    _eq(got["weight_packed"], ref["weight_packed"])
+    _eq(got["weight_scale"], ref["weight_scale"])
+
+
+def test_nvfp4_batched_global_scale(cuda):
+    a = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16,
+                         scale_dtype="float8_e4m3fn")
+    e = torch.stack([_w(32, 128, seed=i, scale=0.01 * (i + 1)) for i in range(3)])
+    got = ops.compress_weight(e.to(cuda), a)
+    for i in range(3):
+        ref = ct.compress_weight(e[i], _oracle_args(a))
+        _eq(got["weight_packed"][i], ref["weight_packed"])
+        _eq(got["weight_scale"][i], ref["weight_scale"])
+        _eq(got["weight_global_scale"][i:i + 1], ref["weight_global_scale"])
+
+
+@pytest.mark.parametrize("scheme", [SCHEMES[0], SCHEMES[3], SCHEMES[11], SCHEMES[15], SCHEMES[17], SCHEMES[18]],
+                         ids=_id)
+def test_dequantize_roundtrip(cuda, scheme):
+    """dequantize(stored codes) == compressed-tensors dequantize of the oracle's codes."""
+    a = QuantizationArgs(**scheme)
+    w = _w(256, 256, seed=5)
+    q = ops.quantize_weight(w.to(cuda), a)
+    d = ops.dequantize(q["codes"], w.shape, a, q["scale"], q["zero_point"], q.get("global_scale"))
+    oa = _oracle_args(a)
+    gs = None
+    if oa.strategy == "tensor_group":
+        gs = ct.generate_gparam(w.amin().reshape(1), w.amax().reshape(1))
+    mn, mx = ct.observe_minmax(w, oa)
+    s, z = ct.calculate_qparams(mn, mx, oa, global_scale=gs)
+    if oa.type == "int":
+        codes = ct.quantize(w, s, z, oa, dtype=torch.int8)
+    elif oa.num_bits == 8:
+        codes = ct.quantize(w, s, z, oa, dtype=torch.float8_e4m3fn)
+    else:
+        codes = ct.quantize(w, s, z, oa, global_scale=gs)
+    _eq(d, ct.dequantize(codes, s, z, oa, dtype=torch.bfloat16, global_scale=gs))
+
+
+def test_observe_qparams_quantize_pipeline(cuda):
+    """observe -> calculate_qparams -> quantize(given qparams) == fused qz_quantize."""
+    for scheme in (SCHEMES[0], SCHEMES[3], SCHEMES[11], SCHEMES[15], SCHEMES[17]):
+        a = QuantizationArgs(**scheme)
+        w = _edge_weight(256, 512, 32).to(cuda)
+        mn, mx = ops.observe_minmax(w, a)
+        s, z = ops.calculate_qparams(mn, mx, a)
+        codes = ops.quantize(w, s, z, a)
+        fused = ops.quantize_weight(w, a)
+        _eq(codes, fused["codes"])
+        _eq(s, fused["scale"])
+
+
+def test_pack_to_int32_both_dims(cuda):
+    g = torch.Generator().manual_seed(0)
+    for bits in (2, 3, 4, 8):
+        v = torch.randint(-(1 << (bits - 1)), 1 << (bits - 1), (37, 53), generator=g).to(torch.int8)
+        for dim in (0, 1):
+            _eq(ops.pack_to_int32(v.to(cuda), bits, dim), ct.pack_to_int32(v, bits, dim))
+
+
+def test_errors_are_value_errors(cuda):
+    w = _w(16, 100).to(cuda)
+    with pytest.raises(ValueError):
+        ops.quantize_weight(w, QuantizationArgs(num_bits=4, group_size=128))
+    with pytest.raises(ValueError):
+        ops.quantize_weight(_w(100, 128).to(cuda), QuantizationArgs(num_bits=8, type="float", strategy="block",
+                                                                     block_structure=[128, 128]))
+
+
+def test_awq_stats(cuda):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 257, 2560, generator=g).to(torch.bfloat16)
+    sums = torch.zeros(2560, dtype=torch.float32, device=cuda)
+    n = ops.awq_absmean_accum(x.to(cuda), sums)
+    assert n == 3 * 257
+    ref, cnt = ct.awq_accumulate_mean(x)
+    torch.testing.assert_close(sums.cpu(), ref, rtol=1e-5, atol=1e-4)
+    ws = [_w(320, 512, seed=i) for i in range(2)]
+    wsum = torch.zeros(512, dtype=torch.float64, device=cuda)
+    rows = sum(ops.awq_weight_mean_accum(w.to(cuda), 32, wsum) for w in ws)
+    ref = ct.awq_layer_means(ws, ct.QArgs(group_size=32))
+    torch.testing.assert_close(wsum.cpu() / rows, ref, rtol=1e-12, atol=1e-12)
+    xm = (ref.float() + 0.1)
+    for ratio in (0.0, 0.35, 0.95):
+        got = ops.awq_grid_scales(xm.to(cuda), ref.to(cuda), ratio, True)
+        torch.testing.assert_close(got.cpu(), ct.awq_grid_scales(xm, ref, ratio, True), rtol=2e-6, atol=1e-7)
+
+
+def test_smoothing_ops(cuda):
+    w = _w(64, 128, seed=2)
+    s = torch.rand(128, generator=torch.Generator().manual_seed(1)) + 0.5
+    got = ops.scale_columns_(w.clone().to(cuda), s.to(cuda))
+    _eq(got, (w.float() * s.view(1, -1)).to(torch.bfloat16))
+    n = _w(1, 128, seed=4).reshape(-1)
+    got = ops.scale_rows_(n.clone().to(cuda), s.to(cuda), divide=True)
+    _eq(got, (n.float() / s).to(torch.bfloat16))
