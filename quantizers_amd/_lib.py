@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libquantizers_amd.so")
+# QUANTIZERS_AMD_LIB overrides the path (tuning builds under scripts/tune_fast.sh only)
+LIB_PATH = os.environ.get("QUANTIZERS_AMD_LIB") or os.path.join(_HERE, "libquantizers_amd.so")
 
 # enums (include/quantizers_amd.h)
 QZ_INT, QZ_FLOAT = 0, 1

@@ -22,6 +22,8 @@ struct QP {
   float qmin, qmax;   // calculate_range
   float half_range;   // (qmax - qmin) / 2  (symmetric scale divisor)
   float range;        // qmax - qmin        (asymmetric scale divisor)
+  float inv_half;     // f32(1 / half_range), correctly rounded (host)
+  float inv_range;    // f32(1 / range)
   float magic;        // 2^23 - qmin: t + magic has RNE(t) - qmin in its low mantissa bits
   int bits;
   int sym;
@@ -109,6 +111,16 @@ __device__ __forceinline__ float mx_pow2(int e) {
   return e >= -126 ? __uint_as_float((uint32_t)(e + 127) << 23) : __uint_as_float(0x00400000u);
 }
 
+// bf16(a / b) for a bf16 value a and a divisor b of <= 8 significant bits, given rb within
+// 1 ulp of 1/b: equal to the IEEE quotient rounded to bf16 whenever the quotient is normal
+// (rcp lemma); tiny / huge / non-finite quotients take the IEEE division.
+__device__ __forceinline__ float bf16_quot(float a, float b, float rb) {
+  float q = a * rb;
+  const float aq = fabsf(q);
+  if (__builtin_expect(!(aq >= 0x1.0p-120f && aq <= 0x1.0p+120f), 0)) q = a / b;
+  return bfr(q);
+}
+
 // ------------------------------------------------------------- per-group params
 struct GP {
   float s;      // dense scale (bf16 value, 2^k for MX, f32 for NV)
@@ -140,12 +152,15 @@ __device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, floa
   float s;
   if (p.sym) {
     float am = fmaxf(fabsf(lo), fabsf(hi));
-    s = bfr(am / p.half_range);
+    s = (am == 0.f) ? 0.f : bf16_quot(am, p.half_range, p.inv_half);
   } else {
-    s = bfr(bfr(hi - lo) / p.range);
-    float t = bfr(lo / s);
+    const float rng = bfr(hi - lo);
+    s = (rng == 0.f) ? 0.f : bf16_quot(rng, p.range, p.inv_range);
+    float t = (s == 0.f || lo == 0.f) ? lo / s : bf16_quot(lo, s, __builtin_amdgcn_rcpf(s));
     g.zp = clamp_t(bfr(p.qmin - t), p.qmin, p.qmax);
-    g.zp = (g.zp != g.zp) ? 0.f : __builtin_rintf(g.zp);  // D10: NaN zp -> 0
+    // D10: NaN zp -> 0.  "+ 0.0f" turns rint's -0 into +0: the reference's zero point is an
+    // int8, and a -0 zp would flip the sign of an exactly-zero fake-quant result
+    g.zp = (g.zp != g.zp) ? 0.f : __builtin_rintf(g.zp) + 0.0f;
   }
   if (p.kind == K_NV) {
     float s32 = gs * s;

@@ -22,21 +22,49 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-constexpr int UNROLL = 4;  // 16-B loads in flight per lane
+#ifndef QZ_UNROLL
+#define QZ_UNROLL 2
+#endif
+constexpr int UNROLL = QZ_UNROLL;  // 16-B loads per lane per tile (x2 in flight when pipelined)
+#ifndef QZ_NUM_CUS
+#define QZ_NUM_CUS 256  // MI355X
+#endif
 
 // ------------------------------------------------------------------------ helpers
-__device__ __forceinline__ void unpack8(const uint4& v, float* x) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    x[2 * k] = __uint_as_float(w[k] << 16);
-    x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-  }
-}
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// xor-butterfly reduction over groups of L consecutive lanes.  L <= 16 uses DPP (VALU
+// cross-lane, no LDS round trip): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
+// row_mirror; wider groups fall back to ds_bpermute shuffles.  Reductions run on uint32 keys
+// (order-preserving images of the floats) so no NaN canonicalisation is needed and the DPP
+// move folds into v_max_u32_dpp / v_min_u32_dpp.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);  // full EXEC: every source lane valid
+}
+template <int L>
+__device__ __forceinline__ uint32_t grp_max_u(uint32_t v) {
+  if (L >= 2) v = max(v, dpp<0xB1>(v));
+  if (L >= 4) v = max(v, dpp<0x4E>(v));
+  if (L >= 8) v = max(v, dpp<0x141>(v));
+  if (L >= 16) v = max(v, dpp<0x140>(v));
+#pragma unroll
+  for (int m = 16; m < L; m <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, WAVE));
+  return v;
+}
+template <int L>
+__device__ __forceinline__ uint32_t grp_min_u(uint32_t v) {
+  if (L >= 2) v = min(v, dpp<0xB1>(v));
+  if (L >= 4) v = min(v, dpp<0x4E>(v));
+  if (L >= 8) v = min(v, dpp<0x141>(v));
+  if (L >= 16) v = min(v, dpp<0x140>(v));
+#pragma unroll
+  for (int m = 16; m < L; m <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, WAVE));
+  return v;
+}
+// float helpers for the generic path
 template <int L>
 __device__ __forceinline__ float grp_max(float v) {
 #pragma unroll
@@ -48,6 +76,10 @@ __device__ __forceinline__ float grp_min(float v) {
 #pragma unroll
   for (int m = 1; m < L; m <<= 1) v = fminf(v, __shfl_xor(v, m, WAVE));
   return v;
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
 
 struct FastArgs {
@@ -66,134 +98,267 @@ struct FastArgs {
 };
 
 // --------------------------------------------------------------- single-pass path
-template <int LOGL, int KIND, bool FQ>
-__global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
-  constexpr int L = 1 << LOGL;
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t wave = (int64_t)blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
-  const int64_t base = wave * (UNROLL * WAVE);
-  QP p = A.p;
-  p.kind = KIND;
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifndef QZ_NT_LOADS
+#define QZ_NT_LOADS 0
+#endif
+#ifndef QZ_NT_STORES
+#define QZ_NT_STORES 0
+#endif
 
-  uint4 v[UNROLL];
+// round both lanes of an f32 pair to bf16 (one v_cvt_pk_bf16_f32) and widen back
+__device__ __forceinline__ f32x2 bfr2(f32x2 v) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+  f32x2 r;
+  r.x = __uint_as_float(u << 16);
+  r.y = __uint_as_float(u & 0xffff0000u);
+  return r;
+}
+
+// Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
+template <int LOGL, int KIND, bool FQ>
+__device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
+                                             const int lane) {
+  constexpr int L = 1 << LOGL;
+  const bool valid = unit < A.n_units;  // uniform within a group (groups never straddle)
+  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+  f32x2 x[4];
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    const int64_t unit = base + u * WAVE + lane;
-    v[u] = unit < A.n_units ? *reinterpret_cast<const uint4*>(A.w + unit * 8) : make_uint4(0, 0, 0, 0);
+  for (int k = 0; k < 4; ++k) {
+    x[k].x = __uint_as_float(wd[k] << 16);
+    x[k].y = __uint_as_float(wd[k] & 0xffff0000u);
+  }
+  f32x2 cs[4];
+  if (FQ && A.col_scales) {
+    const int64_t c0 = (unit % A.units_per_row) * 8;
+    const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
+    const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
+    cs[0] = f32x2{c_lo.x, c_lo.y}; cs[1] = f32x2{c_lo.z, c_lo.w};
+    cs[2] = f32x2{c_hi.x, c_hi.y}; cs[3] = f32x2{c_hi.z, c_hi.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = bfr2(x[k] * cs[k]);  // W * s in the weight dtype
   }
 
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    const int64_t unit = base + u * WAVE + lane;
-    const bool valid = unit < A.n_units;  // uniform within a group (groups never straddle)
-    float x[8];
-    unpack8(v[u], x);
-    float cs[8];
+  // ---- observe: memoryless min/max over the group (exact in bf16), on integer keys
+  float mn, mx;
+  if (p.sym) {
+    uint32_t am;
     if (FQ && A.col_scales) {
-      const int64_t c0 = (unit % A.units_per_row) * 8;
-      const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
-      const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
-      cs[0] = c_lo.x; cs[1] = c_lo.y; cs[2] = c_lo.z; cs[3] = c_lo.w;
-      cs[4] = c_hi.x; cs[5] = c_hi.y; cs[6] = c_hi.z; cs[7] = c_hi.w;
+      am = 0;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = bfr(x[i] * cs[i]);  // W * s in the weight dtype
+      for (int k = 0; k < 4; ++k)
+        am = max(am, max(__float_as_uint(x[k].x) & 0x7fffffffu, __float_as_uint(x[k].y) & 0x7fffffffu));
+    } else {  // |bf16| bit patterns, two per dword: v_pk_max_u16 on the raw words
+      const uint32_t m = pk_max_u16(pk_max_u16(wd[0] & 0x7fff7fffu, wd[1] & 0x7fff7fffu),
+                                    pk_max_u16(wd[2] & 0x7fff7fffu, wd[3] & 0x7fff7fffu));
+      am = max(m & 0xffffu, m >> 16) << 16;
     }
-
-    // ---- observe: memoryless min/max over the group (exact in bf16)
-    float mn, mx;
-    if (p.sym) {
-      float am = fabsf(x[0]);
+    am = grp_max_u<L>(am);
+    mx = __uint_as_float(am);
+    mn = -mx;
+  } else {
+    uint32_t kmn = 0xffffffffu, kmx = 0u;
 #pragma unroll
-      for (int i = 1; i < 8; ++i) am = fmaxf(am, fabsf(x[i]));
-      am = grp_max<L>(am);
-      mn = -am;
-      mx = am;
-    } else {
-      mn = x[0];
-      mx = x[0];
-#pragma unroll
-      for (int i = 1; i < 8; ++i) { mn = fminf(mn, x[i]); mx = fmaxf(mx, x[i]); }
-      mn = grp_min<L>(mn);
-      mx = grp_max<L>(mx);
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a = f2key(x[k].x), b = f2key(x[k].y);
+      kmn = min(kmn, min(a, b));
+      kmx = max(kmx, max(a, b));
     }
-    float gs = 0.f;
-    if (KIND == K_NV) gs = A.gscale[valid ? unit / A.units_per_batch : 0];
-    const GP g = group_params(p, mn, mx, gs);
+    mn = key2f(grp_min_u<L>(kmn));
+    mx = key2f(grp_max_u<L>(kmx));
+  }
+  float gs = 0.f;
+  if (KIND == K_NV) gs = A.gscale[valid ? unit / A.units_per_batch : 0];
+  const GP g = group_params(p, mn, mx, gs);
 
-    // ---- quotient x / scale (bf16; f32 for NVFP4)
-    float t[8];
-    if (KIND == K_NV) {
+  // ---- quotient x / scale (bf16; f32 for NVFP4); x * rcp(s) is exact-equivalent (rcp lemma)
+  f32x2 t[4];
+  if (KIND == K_NV) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = x[i] / g.s;
-    } else {
+    for (int k = 0; k < 4; ++k) { t[k].x = x[k].x / g.s; t[k].y = x[k].y / g.s; }
+  } else {
+    const f32x2 rs2 = {g.rs, g.rs};
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = x[i] * g.rs;
-      if (__builtin_expect(!g.fast, 0)) {
+    for (int k = 0; k < 4; ++k) t[k] = x[k] * rs2;
+    if (__builtin_expect(!g.fast, 0)) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) t[i] = x[i] / g.s;
+      for (int k = 0; k < 4; ++k) { t[k].x = x[k].x / g.s; t[k].y = x[k].y / g.s; }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = bfr2(t[k]);
+  }
+  if (!valid) return;
+
+  if (KIND == K_INT) {
+    // clamp (bf16 bounds), then t + (2^23 - qmin): RNE(t) - qmin lands in the low mantissa bits
+    f32x2 q[4];
+    const f32x2 mg = {p.magic, p.magic};
+    const f32x2 zp2 = {g.zp, g.zp};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x2 tk = t[k];
+      if (!p.sym) tk = bfr2(tk + zp2);
+      tk.x = __builtin_amdgcn_fmed3f(tk.x, p.qmin, p.qmax);
+      tk.y = __builtin_amdgcn_fmed3f(tk.y, p.qmin, p.qmax);
+      t[k] = tk;
+      q[k] = tk + mg;
+    }
+    if (FQ) {
+      float d[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // round() keeps the sign of zero (-0 dequantizes to -0)
+        d[2 * k] = bfr(bfr(__builtin_rintf(t[k].x) - g.zp) * g.s);
+        d[2 * k + 1] = bfr(bfr(__builtin_rintf(t[k].y) - g.zp) * g.s);
       }
+      if (A.col_scales) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = bfr(t[i]);
+        for (int k = 0; k < 4; ++k) { d[2 * k] = bfr(d[2 * k] / cs[k].x); d[2 * k + 1] = bfr(d[2 * k + 1] / cs[k].y); }
+      }
+      uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
+      reinterpret_cast<uint4*>(A.q_out)[unit] = o;
+    } else if (A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
+      // word = sum_i (0x4B000000 + u_i) << 4i  - 0xFB000000   (mod 2^32): one shift-add per code
+      uint32_t acc = 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc += __float_as_uint(q[k].x) << (8 * k);
+        acc += __float_as_uint(q[k].y) << (8 * k + 4);
+      }
+      reinterpret_cast<uint32_t*>(A.q_out)[unit] = acc - 0xFB000000u;
+    } else {
+      uint32_t c[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        c[2 * k] = __float_as_uint(q[k].x) & 0xffu;
+        c[2 * k + 1] = __float_as_uint(q[k].y) & 0xffu;
+      }
+      if (A.out_fmt == QZ_OUT_PACKED_INT32) {  // 8 bits: u = q + 128, 4 per word
+        reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+      } else {  // int8 (signed) bytes
+        const uint32_t off = (uint32_t)(-(int)p.qmin);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) c[i] = (c[i] - off) & 0xffu;
+        reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+      }
     }
-
-    // ---- round / clamp / encode
+  } else {
     uint32_t c[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float ti = t[i];
-      if (KIND == K_INT) {
-        if (!p.sym) ti = bfr(ti + g.zp);
-        ti = clamp_t(ti, p.qmin, p.qmax);
-        t[i] = ti;  // kept for fake-quant: round() keeps the sign of zero
-        c[i] = (ti != ti) ? (uint32_t)(-(int)p.qmin)
-                          : (__float_as_uint(ti + p.magic) & ((1u << p.bits) - 1u));
-      } else if (KIND == K_FP8) {
-        c[i] = bf16_to_e4m3(f2bf(clamp_t(ti, -448.f, 448.f)));
+    for (int k = 0; k < 4; ++k) {
+      if (KIND == K_FP8) {
+        c[2 * k] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f)));
+        c[2 * k + 1] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f)));
       } else {
-        c[i] = fp4_code(clamp_t(ti, -6.f, 6.f));
+        c[2 * k] = fp4_code(__builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f));
+        c[2 * k + 1] = fp4_code(__builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f));
       }
     }
-
-    if (!valid) continue;
     if (FQ) {
       float d[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        d[i] = (KIND == K_INT) ? bfr(bfr(__builtin_rintf(t[i]) - g.zp) * g.s) : decode(p, g, c[i]);
-        if (A.col_scales) d[i] = bfr(d[i] / cs[i]);
+        d[i] = decode(p, g, c[i]);
+        if (A.col_scales) d[i] = bfr(d[i] / ((i & 1) ? cs[i >> 1].y : cs[i >> 1].x));
       }
       uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
       reinterpret_cast<uint4*>(A.q_out)[unit] = o;
-    } else if (KIND == K_INT && A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
-      uint32_t word = 0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) word |= c[i] << (4 * i);
-      reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
-    } else if (KIND == K_INT && A.out_fmt == QZ_OUT_PACKED_INT32) {  // 8 bits: 2 words
-      uint2 o = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
-                           c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
-      reinterpret_cast<uint2*>(A.q_out)[unit] = o;
-    } else if (KIND == K_INT || KIND == K_FP8) {  // int8 / e4m3 bytes
-      uint32_t off = (KIND == K_INT) ? (uint32_t)(-(int)p.qmin) : 0u;
-      uint32_t b[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) b[i] = (c[i] - off) & 0xffu;
-      uint2 o = make_uint2(b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24),
-                           b[4] | (b[5] << 8) | (b[6] << 16) | (b[7] << 24));
-      reinterpret_cast<uint2*>(A.q_out)[unit] = o;
+    } else if (KIND == K_FP8) {
+      reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                           c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
     } else {  // fp4 packed: element 2k in the low nibble of byte k
       uint32_t word = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) word |= c[i] << (4 * i);
       reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
     }
-    if ((lane & (L - 1)) == 0) {
-      const int64_t gi = unit >> LOGL;
-      if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
-      else reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
-      if (A.zp_out) A.zp_out[gi] = (int8_t)g.zp;
-    }
   }
+  if ((lane & (L - 1)) == 0) {
+    const int64_t gi = unit >> LOGL;
+    if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
+    else reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
+    if (A.zp_out) A.zp_out[gi] = (int8_t)g.zp;
+  }
+}
+
+// branch-free: out-of-range lanes re-load the last unit (their results are never stored)
+__device__ __forceinline__ void load_tile(const FastArgs& A, int64_t tile, int lane, uint4* v) {
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+    unit = unit < A.n_units ? unit : A.n_units - 1;
+#if QZ_NT_LOADS
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(A.w) + unit);
+    v[u] = make_uint4(t.x, t.y, t.z, t.w);
+#else
+    v[u] = reinterpret_cast<const uint4*>(A.w)[unit];
+#endif
+  }
+}
+
+template <int LOGL, int KIND, bool FQ>
+__device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t tile, int lane) {
+#ifdef QZ_TUNE_WIDE_STORE  // probe: one 16-B store per lane per tile (UNROLL == 4)
+  {
+    uint32_t h[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) h[u] = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    const int64_t w0 = tile * (UNROLL * WAVE) + 4 * lane;
+    if (w0 < A.n_units) {
+#if QZ_NT_STORES
+      __builtin_nontemporal_store(u32x4{h[0], h[1], h[2], h[3]}, reinterpret_cast<u32x4*>(A.q_out) + (w0 >> 2));
+#else
+      reinterpret_cast<uint4*>(A.q_out)[w0 >> 2] = make_uint4(h[0], h[1], h[2], h[3]);
+#endif
+      if (lane < 2) reinterpret_cast<uint4*>(A.s_out)[(tile * (UNROLL * WAVE) >> 4) / 8 + lane] = make_uint4(h[0], h[1], h[2], h[3]);
+    }
+    return;
+  }
+#endif
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+#ifdef QZ_TUNE_NULL_COMPUTE  // tuning probe only: same traffic, no arithmetic
+    const int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+    const uint32_t h = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+#if defined(QZ_TUNE_NO_STORE)
+    if (h == 0x12345679u && lane == 63) reinterpret_cast<uint32_t*>(A.q_out)[0] = h;
+#else
+    if (unit < A.n_units) {
+#if QZ_NT_STORES
+      __builtin_nontemporal_store(h, reinterpret_cast<uint32_t*>(A.q_out) + unit);
+#else
+      reinterpret_cast<uint32_t*>(A.q_out)[unit] = h;
+#endif
+#ifndef QZ_TUNE_NO_SCALE_STORE
+      if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
+#endif
+    }
+#endif
+#else
+    process_unit<LOGL, KIND, FQ>(A, p, v[u], tile * (UNROLL * WAVE) + u * WAVE + lane, lane);
+#endif
+  }
+}
+
+// One tile (UNROLL*64 units = UNROLL KiB of bf16) per wave, all UNROLL 16-B loads issued
+// before any arithmetic; latency is hidden by occupancy (up to 8 waves per SIMD).  Measured
+// on MI355X this beats a persistent grid-stride loop with register double-buffering (the
+// VALU-heavy waves need other resident waves to overlap with, not deeper per-wave queues).
+template <int LOGL, int KIND, bool FQ>
+__global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t tile = (int64_t)blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+  const int64_t n_tiles = (A.n_units + UNROLL * WAVE - 1) / (UNROLL * WAVE);
+  if (tile >= n_tiles) return;
+  QP p = A.p;
+  p.kind = KIND;
+  uint4 v[UNROLL];
+  load_tile(A, tile, lane, v);
+  process_tile<LOGL, KIND, FQ>(A, p, v, tile, lane);
 }
 
 // ------------------------------------------------------------------ generic path
@@ -476,6 +641,8 @@ int make_plan(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
   p.kind = pl->kind;
   p.half_range = (p.qmax - p.qmin) / 2.0f;
   p.range = p.qmax - p.qmin;
+  p.inv_half = 1.0f / p.half_range;
+  p.inv_range = 1.0f / p.range;
   p.magic = 8388608.0f - p.qmin;
   pl->scale_fmt = a->scale_fmt;
   pl->scale_bytes = (a->scale_fmt == QZ_SCALE_NATIVE) ? 2 : 1;
@@ -658,8 +825,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.col_scales = col_scales;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
-    const int64_t waves = cdiv(F.n_units, UNROLL * WAVE);
-    const int64_t blocks = cdiv(waves, BLOCK / WAVE);
+    const int64_t n_tiles = cdiv(F.n_units, UNROLL * WAVE);
+    const int64_t blocks = cdiv(n_tiles, BLOCK / WAVE);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, fq), dim3((unsigned)blocks), dim3(BLOCK), 0, st, F);
     return launch_err();
   }

@@ -144,8 +144,8 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
         o["codes"] = _alloc_codes(out_fmt, a, lead, r, c, dev)
     if "scale" not in o:
         o["scale"] = torch.empty(*lead, *gshape, dtype=_scale_dtype(a), device=dev)
-    if "zero_point" not in o:
-        o["zero_point"] = torch.empty(*lead, *gshape, dtype=torch.int8, device=dev)
+    if "zero_point" not in o:  # symmetric: no zero-point tensor (compressed-tensors stores none)
+        o["zero_point"] = None if a.symmetric else torch.empty(*lead, *gshape, dtype=torch.int8, device=dev)
     if a.is_nvfp4 and "global_scale" not in o:
         o["global_scale"] = torch.empty(max(b, 1), dtype=torch.float32, device=dev)
     lib = _lib.load()

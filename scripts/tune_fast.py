@@ -1,0 +1,109 @@
+"""Interleaved A/B timing of library build variants (one process, rounds interleaved).
+usage: python scripts/tune_fast.py build/tune/libqz_a.so build/tune/libqz_b.so ..."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from quantizers_amd import _lib  # noqa: E402
+
+ROWS, COLS = int(os.environ.get("ROWS", 11008)), int(os.environ.get("COLS", 4096))
+G = int(os.environ.get("GROUP", 128))
+BITS = int(os.environ.get("BITS", 4))
+KIND = os.environ.get("KIND", "int")
+COPIES = int(os.environ.get("COPIES", 12))
+P = ctypes.c_void_p
+
+
+def load(path):
+    lib = ctypes.CDLL(path)
+    lib.qz_quantize.argtypes = [P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                ctypes.POINTER(_lib.QzArgs), ctypes.c_int32, P, P, P, P, P, ctypes.c_size_t, P]
+    lib.qz_quantize_workspace_size.argtypes = [ctypes.c_int64] * 3 + [ctypes.POINTER(_lib.QzArgs)]
+    lib.qz_quantize_workspace_size.restype = ctypes.c_size_t
+    return lib
+
+
+def main():
+    paths = sys.argv[1:]
+    libs = [load(p) for p in paths]
+    dev = torch.device("cuda:0")
+    ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
+    if KIND == "int":
+        a = _lib.QzArgs(BITS, 0, 1, 2, G, 0, 0, 0)
+        fmt = 0
+        codes = torch.empty(ROWS, COLS * BITS // 32, dtype=torch.int32, device=dev)
+        scale = torch.empty(ROWS, COLS // G, dtype=torch.bfloat16, device=dev)
+    elif KIND == "fp8":
+        a = _lib.QzArgs(8, 1, 1, 2, G, 0, 0, 0)
+        fmt = 2
+        codes = torch.empty(ROWS, COLS, dtype=torch.uint8, device=dev)
+        scale = torch.empty(ROWS, COLS // G, dtype=torch.bfloat16, device=dev)
+    else:  # mx
+        a = _lib.QzArgs(4, 1, 1, 2, 32, 0, 0, 3)
+        fmt = 3
+        codes = torch.empty(ROWS, COLS // 2, dtype=torch.uint8, device=dev)
+        scale = torch.empty(ROWS, COLS // 32, dtype=torch.uint8, device=dev)
+    n = libs[0].qz_quantize_workspace_size(1, ROWS, COLS, ctypes.byref(a))
+    wsp = torch.empty(n + 256, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    sp = P(st.cuda_stream)
+    ref = None
+
+    def run(lib, i):
+        rc = lib.qz_quantize(P(ws[i % COPIES].data_ptr()), 1, ROWS, COLS, COLS, ROWS * COLS, ctypes.byref(a), fmt,
+                             P(codes.data_ptr()), P(scale.data_ptr()), P(0), P(0), P(wsp.data_ptr()), wsp.numel(), sp)
+        assert rc == 0, rc
+
+    for lib in libs:  # correctness: every variant gives identical bits
+        run(lib, 0)
+        torch.cuda.synchronize()
+        cur = (codes.clone(), scale.clone())
+        if ref is None:
+            ref = cur
+        else:
+            same = torch.equal(ref[0], cur[0]) and torch.equal(ref[1].view(torch.int16), cur[1].view(torch.int16))
+            if not same:
+                print(f"NOTE: {lib._name} output differs from {paths[0]} (expected only for probe builds)")
+    K = 60
+    res = {p: [] for p in paths}
+    for rnd in range(8):
+        for p, lib in zip(paths, libs):
+            for i in range(10):
+                run(lib, i)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+            for i in range(K):
+                ev[i][0].record(st)
+                run(lib, i)
+                ev[i][1].record(st)
+            torch.cuda.synchronize()
+            d = sorted(s.elapsed_time(e) * 1e3 for s, e in ev)
+            res[p].append(d[K // 2])
+    # reference points: torch copy (read+write 2x90 MB) and a read-only sum over one copy
+    src = ws[0]
+    dst = torch.empty_like(src)
+    for name, fn, nbytes in [("torch.copy_ bf16", lambda i: dst.copy_(ws[i % COPIES]), 2 * src.numel() * 2),
+                             ("torch.sum (read)", lambda i: ws[i % COPIES].sum(dtype=torch.float32),
+                              src.numel() * 2)]:
+        for i in range(10):
+            fn(i)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        for i in range(K):
+            ev[i][0].record(st)
+            fn(i)
+            ev[i][1].record(st)
+        torch.cuda.synchronize()
+        d = sorted(s.elapsed_time(e) * 1e3 for s, e in ev)
+        print(f"{name:28s} median {d[K//2]:7.2f} us  -> {nbytes / (d[K//2] * 1e-6) / 1e9:7.0f} GB/s")
+    alg = ROWS * COLS * 2 + ROWS * COLS * BITS // 8 + ROWS * COLS // G * 2
+    for p in paths:
+        v = sorted(res[p])
+        print(f"{os.path.basename(p):28s} median {v[len(v)//2]:7.2f} us  min {v[0]:7.2f} us  "
+              f"-> {alg / (v[len(v)//2] * 1e-6) / 1e9:7.0f} GB/s alg ({KIND})")
+
+
+if __name__ == "__main__":
+    main()
