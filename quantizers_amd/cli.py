@@ -1,0 +1,107 @@
+"""``do_oneshot`` CLI: the reference's scripts/do_oneshot.py surface (same flags, same YAML keys,
+same output-directory rule) on the MI355X path.
+
+Reference flags (scripts/do_oneshot.py:47-79): --config, --output, --cache-dir, --log-file,
+--debug.  Offline additions (no Hub access in this environment): --model-path (a local HF model
+directory instead of ``model.name``), --random-init (build ``model.name``'s architecture from a
+local config with random weights), --calib-file (tokenized calibration set: .pt tensor
+[N, S] or .jsonl rows with ``input_ids``) and --calib-random N,S (synthetic token ids).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+from typing import Optional
+
+import torch
+
+
+def setup_logging(log_file: Optional[str] = None, level: int = logging.INFO):
+    handlers = [logging.StreamHandler(sys.stdout)]
+    if log_file:
+        handlers.append(logging.FileHandler(log_file))
+    logging.basicConfig(level=level, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s",
+                        handlers=handlers, force=True)
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="Calibration-based quantization entry point (MI355X)")
+    p.add_argument("--config", type=str, required=True, help="Path to quantization configuration file")
+    p.add_argument("--output", type=str, required=False, help="Output directory for quantized model")
+    p.add_argument("--cache-dir", type=str, default="./cache", help="Directory to cache calibration sets")
+    p.add_argument("--log-file", type=str, default=None, help="Path to log file (default: stdout only)")
+    p.add_argument("--debug", action="store_true", help="Enable debug logging")
+    p.add_argument("--model-path", type=str, default=None, help="local model directory (offline)")
+    p.add_argument("--random-init", type=str, default=None,
+                   help="HF config.json (file or dir) to build a random-weight model from")
+    p.add_argument("--calib-file", type=str, default=None)
+    p.add_argument("--calib-random", type=str, default=None, help="N,S synthetic calibration tokens")
+    p.add_argument("--max-seq-length", type=int, default=None)
+    p.add_argument("--device", type=str, default=None)
+    return p.parse_args(argv)
+
+
+def _calibration(args, run, vocab: int):
+    if args.calib_file:
+        if args.calib_file.endswith(".pt"):
+            t = torch.load(args.calib_file, weights_only=True)
+            return [{"input_ids": r} for r in t]
+        rows = []
+        with open(args.calib_file) as f:
+            for line in f:
+                rows.append(json.loads(line))
+        return rows
+    if args.calib_random:
+        n, s = (int(x) for x in args.calib_random.split(","))
+        g = torch.Generator().manual_seed(42)  # reference shuffle seed (calibration_sets.py:618-619)
+        return [{"input_ids": torch.randint(0, vocab, (s,), generator=g)} for _ in range(n)]
+    return None
+
+
+def load_model(args, run):
+    from transformers import AutoConfig, AutoModelForCausalLM
+    if args.random_init:
+        cfg = AutoConfig.from_pretrained(args.random_init)
+        torch.manual_seed(0)
+        return AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    path = args.model_path or run.model.name
+    return AutoModelForCausalLM.from_pretrained(path, dtype=torch.bfloat16, low_cpu_mem_usage=True,
+                                                trust_remote_code=True)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    setup_logging(args.log_file, logging.DEBUG if args.debug else logging.INFO)
+    from .config import load_run_config
+    from .oneshot import oneshot
+    from .compressor import save_compressed
+
+    logging.info("Loading configuration from: %s", args.config)
+    run = load_run_config(args.config)
+    output_dir = args.output or run.output_dir()
+    recipe_path = run.resolve_recipe()
+    model = load_model(args, run)
+    vocab = getattr(model.config, "vocab_size", 32000)
+    dataset = _calibration(args, run, vocab)
+    max_len = args.max_seq_length or (run.calibration or {}).get("max_seq_length", 2048)
+    logging.info("Starting quantization")
+    t0 = time.time()
+    oneshot(model=model, recipe=recipe_path, dataset=dataset, max_seq_length=max_len,
+            num_calibration_samples=len(dataset) if dataset else None, moe_calibrate_all_experts=True,
+            device=args.device)
+    logging.info("Completed quantization in %.2f seconds", time.time() - t0)
+    os.makedirs("outputs", exist_ok=True)
+    logging.info("Saving quantized model to: %s", output_dir)
+    t0 = time.time()
+    save_compressed(model, output_dir)
+    logging.info("Saved quantized model in %.2f seconds", time.time() - t0)
+    logging.info("SUCCESS: Quantized model saved in %s", output_dir)
+    return output_dir
+
+
+if __name__ == "__main__":
+    main()

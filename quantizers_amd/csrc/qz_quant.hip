@@ -87,6 +87,7 @@ struct FastArgs {
   int64_t n_units;          // batch*rows*cols/8
   int64_t units_per_batch;  // rows*cols/8
   int64_t units_per_row;    // cols/8
+  int64_t ld_batch;         // elements between batch slices (rows*cols when dense)
   QP p;
   int out_fmt;
   int scale_bytes;  // 2 (bf16) or 1 (e4m3 / e8m0)
@@ -120,9 +121,9 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
 // Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
 template <int LOGL, int KIND, bool FQ>
 __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
-                                             const int lane) {
+                                             const bool valid, const float gs, const int lane) {
   constexpr int L = 1 << LOGL;
-  const bool valid = unit < A.n_units;  // uniform within a group (groups never straddle)
+  // unit: dense output index (batch*units_per_batch + local); valid is uniform within a group
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
   f32x2 x[4];
 #pragma unroll
@@ -169,8 +170,6 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
     mn = key2f(grp_min_u<L>(kmn));
     mx = key2f(grp_max_u<L>(kmx));
   }
-  float gs = 0.f;
-  if (KIND == K_NV) gs = A.gscale[valid ? unit / A.units_per_batch : 0];
   const GP g = group_params(p, mn, mx, gs);
 
   // ---- quotient x / scale (bf16; f32 for NVFP4); x * rcp(s) is exact-equivalent (rcp lemma)
@@ -285,61 +284,38 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
 }
 
-// branch-free: out-of-range lanes re-load the last unit (their results are never stored)
-__device__ __forceinline__ void load_tile(const FastArgs& A, int64_t tile, int lane, uint4* v) {
+// branch-free: out-of-range lanes re-load the slice's last unit (results never stored)
+__device__ __forceinline__ void load_tile(const FastArgs& A, const uint16_t* wb, int64_t tile, int lane, uint4* v) {
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
-    unit = unit < A.n_units ? unit : A.n_units - 1;
+    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
 #if QZ_NT_LOADS
-    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(A.w) + unit);
+    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wb) + unit);
     v[u] = make_uint4(t.x, t.y, t.z, t.w);
 #else
-    v[u] = reinterpret_cast<const uint4*>(A.w)[unit];
+    v[u] = reinterpret_cast<const uint4*>(wb)[unit];
 #endif
   }
 }
 
 template <int LOGL, int KIND, bool FQ>
-__device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t tile, int lane) {
-#ifdef QZ_TUNE_WIDE_STORE  // probe: one 16-B store per lane per tile (UNROLL == 4)
-  {
-    uint32_t h[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) h[u] = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    const int64_t w0 = tile * (UNROLL * WAVE) + 4 * lane;
-    if (w0 < A.n_units) {
-#if QZ_NT_STORES
-      __builtin_nontemporal_store(u32x4{h[0], h[1], h[2], h[3]}, reinterpret_cast<u32x4*>(A.q_out) + (w0 >> 2));
-#else
-      reinterpret_cast<uint4*>(A.q_out)[w0 >> 2] = make_uint4(h[0], h[1], h[2], h[3]);
-#endif
-      if (lane < 2) reinterpret_cast<uint4*>(A.s_out)[(tile * (UNROLL * WAVE) >> 4) / 8 + lane] = make_uint4(h[0], h[1], h[2], h[3]);
-    }
-    return;
-  }
-#endif
+__device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t b, int64_t tile,
+                                             int lane) {
+  const float gs = (KIND == K_NV) ? A.gscale[b] : 0.f;
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
+    const int64_t local = tile * (UNROLL * WAVE) + u * WAVE + lane;
+    const int64_t unit = b * A.units_per_batch + local;
+    const bool valid = local < A.units_per_batch;
 #ifdef QZ_TUNE_NULL_COMPUTE  // tuning probe only: same traffic, no arithmetic
-    const int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
     const uint32_t h = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-#if defined(QZ_TUNE_NO_STORE)
-    if (h == 0x12345679u && lane == 63) reinterpret_cast<uint32_t*>(A.q_out)[0] = h;
-#else
-    if (unit < A.n_units) {
-#if QZ_NT_STORES
-      __builtin_nontemporal_store(h, reinterpret_cast<uint32_t*>(A.q_out) + unit);
-#else
+    if (valid) {
       reinterpret_cast<uint32_t*>(A.q_out)[unit] = h;
-#endif
-#ifndef QZ_TUNE_NO_SCALE_STORE
       if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
-#endif
     }
-#endif
 #else
-    process_unit<LOGL, KIND, FQ>(A, p, v[u], tile * (UNROLL * WAVE) + u * WAVE + lane, lane);
+    process_unit<LOGL, KIND, FQ>(A, p, v[u], unit, valid, gs, lane);
 #endif
   }
 }
@@ -348,17 +324,19 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
 // before any arithmetic; latency is hidden by occupancy (up to 8 waves per SIMD).  Measured
 // on MI355X this beats a persistent grid-stride loop with register double-buffering (the
 // VALU-heavy waves need other resident waves to overlap with, not deeper per-wave queues).
+// grid = (tiles per slice, batch): batch slices may be strided (fused-expert views).
 template <int LOGL, int KIND, bool FQ>
 __global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
   const int lane = threadIdx.x & (WAVE - 1);
   const int64_t tile = (int64_t)blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
-  const int64_t n_tiles = (A.n_units + UNROLL * WAVE - 1) / (UNROLL * WAVE);
-  if (tile >= n_tiles) return;
+  const int64_t tiles = (A.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
+  if (tile >= tiles) return;
+  const int64_t b = blockIdx.y;
   QP p = A.p;
   p.kind = KIND;
   uint4 v[UNROLL];
-  load_tile(A, tile, lane, v);
-  process_tile<LOGL, KIND, FQ>(A, p, v, tile, lane);
+  load_tile(A, A.w + b * A.ld_batch, tile, lane, v);
+  process_tile<LOGL, KIND, FQ>(A, p, v, b, tile, lane);
 }
 
 // ------------------------------------------------------------------ generic path
@@ -785,6 +763,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
   if (!ws || ws_bytes < ws_size(batch, pl)) return QZ_ERR_WORKSPACE;
   const WS W = ws_layout(ws, batch, pl);
   const bool contig = ld_row == cols && (batch == 1 || ld_batch == rows * cols);
+  const bool rows_dense = ld_row == cols && (batch == 1 || ld_batch % 8 == 0);  // fast path: per-slice dense
   if (fq && q_out == w && !contig) return QZ_ERR_FORMAT;  // in place only when dense
   // fake-quant keeps its qparams in the workspace
   void* s_dst = scale_out ? scale_out : W.scale;
@@ -809,12 +788,13 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
   const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
   const bool pack_ok = !(pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits != 4 && a->num_bits != 8);
   const bool al = aligned(w, 16) && aligned(q_out, fq ? 16 : 8) && (!col_scales || aligned(col_scales, 16));
-  if (grp && pow2 && contig && pack_ok && al) {
+  if (grp && pow2 && rows_dense && pack_ok && al && batch <= 65535) {
     FastArgs F;
     F.w = (const uint16_t*)w;
     F.n_units = batch * rows * cols / 8;
     F.units_per_batch = rows * cols / 8;
     F.units_per_row = cols / 8;
+    F.ld_batch = batch > 1 ? ld_batch : rows * cols;
     F.p = pl.p;
     F.out_fmt = out_fmt;
     F.scale_bytes = pl.scale_bytes;
@@ -825,9 +805,9 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.col_scales = col_scales;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
-    const int64_t n_tiles = cdiv(F.n_units, UNROLL * WAVE);
+    const int64_t n_tiles = cdiv(F.units_per_batch, UNROLL * WAVE);
     const int64_t blocks = cdiv(n_tiles, BLOCK / WAVE);
-    hipLaunchKernelGGL(pick_fast(logl, pl.kind, fq), dim3((unsigned)blocks), dim3(BLOCK), 0, st, F);
+    hipLaunchKernelGGL(pick_fast(logl, pl.kind, fq), dim3((unsigned)blocks, (unsigned)batch), dim3(BLOCK), 0, st, F);
     return launch_err();
   }
 

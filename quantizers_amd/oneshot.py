@@ -1,0 +1,172 @@
+"""``oneshot`` -- drop-in for the ``llmcompressor.oneshot`` call the reference makes at
+scripts/do_oneshot.py:179-187, plus ``save_compressed`` for ``model.save_pretrained(...,
+save_compressed=True)`` (scripts/do_oneshot.py:197).
+
+Flow, one process per GPU:
+  recipe -> modifiers -> per-module schemes (targets / ignore)
+  [AWQ] layer-sequential calibration: capture layer-0 inputs, then per decoder layer:
+        onload -> statistics + grid search + smoothing (awq.py) -> propagate outputs -> offload
+  quantization state: every targeted weight gets its scheme; the compressed tensors are
+        produced by the fused HIP kernel (ops.compress_weight) at save time or on demand.
+The returned model keeps bf16 (smoothed) weights; ``model.quantization_scheme_map`` names the
+scheme of each targeted module (same names as the reference's per-expert Linear layout).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
+
+import torch
+from torch import nn
+
+from . import awq as awq_mod
+from .model import LinearRef, decoder_layers, iter_linears
+from .quantization import QuantizationArgs, QuantizationScheme
+from .recipe import AWQModifier, QuantizationModifier, match_any, parse_recipe
+
+log = logging.getLogger(__name__)
+
+
+class _StopForward(Exception):
+    pass
+
+
+def resolve_schemes(model: nn.Module, modifiers: List[QuantizationModifier]) -> Dict[str, Tuple[QuantizationScheme, QuantizationModifier]]:
+    """module name -> (scheme, owning modifier); later modifiers do not override earlier ones."""
+    out: Dict[str, Tuple[QuantizationScheme, QuantizationModifier]] = {}
+    refs = iter_linears(model)
+    for mod in modifiers:
+        for ref in refs:
+            if ref.name in out:
+                continue
+            if match_any(ref.name, ref.type_name, mod.ignore):
+                continue
+            for scheme in mod.config_groups.values():
+                if scheme.weights is None:
+                    continue
+                if match_any(ref.name, ref.type_name, scheme.targets):
+                    out[ref.name] = (scheme, mod)
+                    break
+    return out
+
+
+def _batches(dataset, num_samples: Optional[int], max_seq_length: Optional[int], device) -> List[Dict[str, torch.Tensor]]:
+    """Tokenized dataset (HF Dataset / list of dicts / tensor) -> list of batch-1 model inputs."""
+    if dataset is None:
+        return []
+    rows: Iterable
+    if torch.is_tensor(dataset):
+        rows = [{"input_ids": r} for r in dataset]
+    else:
+        rows = dataset
+    out = []
+    for i, r in enumerate(rows):
+        if num_samples is not None and i >= num_samples:
+            break
+        ids = r["input_ids"]
+        ids = torch.as_tensor(ids, dtype=torch.long).reshape(1, -1)
+        if max_seq_length:
+            ids = ids[:, :max_seq_length]
+        b = {"input_ids": ids.to(device)}
+        if "attention_mask" in r and r["attention_mask"] is not None:
+            b["attention_mask"] = torch.as_tensor(r["attention_mask"], dtype=torch.long).reshape(1, -1)[:, :ids.shape[1]].to(device)
+        out.append(b)
+    return out
+
+
+@torch.no_grad()
+def _capture_layer0_inputs(model: nn.Module, layers: nn.ModuleList, batches) -> List[Tuple[tuple, dict]]:
+    cached: List[Tuple[tuple, dict]] = []
+
+    def hook(mod, args, kwargs):
+        kw = {k: v for k, v in kwargs.items() if k not in ("past_key_values", "past_key_value", "use_cache")}
+        kw["use_cache"] = False
+        cached.append((args, kw))
+        raise _StopForward
+
+    h = layers[0].register_forward_pre_hook(hook, with_kwargs=True)
+    try:
+        for b in batches:
+            try:
+                model(**b, use_cache=False)
+            except _StopForward:
+                pass
+    finally:
+        h.remove()
+    return cached
+
+
+def _layer_out(o):
+    return o[0] if isinstance(o, tuple) else o
+
+
+@torch.no_grad()
+def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report):
+    layers = decoder_layers(model)
+    lname = next(n for n, m in model.named_modules() if m is layers)
+    weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
+    mappings = awq.mappings or awq_mod.DEFAULT_MAPPINGS
+    inputs = _capture_layer0_inputs(model, layers, batches)
+    for i, layer in enumerate(layers):
+        home = next(layer.parameters()).device
+        layer.to(device)
+        t0 = time.time()
+        rep = awq_mod.awq_layer(layer, f"{lname}.{i}", inputs, mappings, weights, awq.duo_scaling, awq.n_grid)
+        report[f"{lname}.{i}"] = rep
+        nxt = []
+        for args, kwargs in inputs:
+            out = _layer_out(layer(*args, **kwargs))
+            nxt.append(((out,) + tuple(args[1:]), kwargs))
+        inputs = nxt
+        if home != device:
+            layer.to(home)
+        log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), time.time() - t0)
+
+
+def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, processor=None,
+            max_seq_length: Optional[int] = 2048, num_calibration_samples: Optional[int] = 512,
+            moe_calibrate_all_experts: bool = True, device: Union[str, torch.device, None] = None,
+            output_dir: Optional[str] = None, **kwargs) -> nn.Module:
+    """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
+    scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
+    dataset is already tokenized).  MoE routing during calibration follows the model's own
+    router (``moe_calibrate_all_experts`` applies to AWQ over expert layers, which this round
+    does not smooth -- see DESIGN.md)."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    device = torch.device(device)
+    modifiers = parse_recipe(recipe)
+    schemes = resolve_schemes(model, modifiers)
+    if not schemes:
+        raise ValueError("recipe targets no module of this model")
+    report: Dict[str, Any] = {}
+    awqs = [m for m in modifiers if isinstance(m, AWQModifier)]
+    if awqs:
+        batches = _batches(dataset, num_calibration_samples, max_seq_length, device)
+        if not batches:
+            raise ValueError("AWQModifier needs a calibration dataset")
+        if next(model.parameters()).device.type == "cpu":
+            # embeddings / rotary / final norm run on the device; layers are onloaded one by one
+            _to_device_except(model, decoder_layers(model), device)
+        for m in awqs:
+            _sequential_awq(model, m, schemes, batches, device, report)
+    model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
+    model.quantization_modifiers = modifiers
+    model.awq_report = report
+    if output_dir is not None:
+        from .compressor import save_compressed
+        save_compressed(model, output_dir)
+    return model
+
+
+def _to_device_except(model: nn.Module, layers: nn.ModuleList, device):
+    """Move everything but the decoder layers to ``device`` (layers are onloaded one at a time)."""
+    inside = {id(m) for m in layers.modules()}
+    for m in model.modules():
+        if id(m) in inside:
+            continue
+        for p in m.parameters(recurse=False):
+            p.data = p.data.to(device)
+        for k, b in list(m.named_buffers(recurse=False)):
+            setattr(m, k, b.to(device))

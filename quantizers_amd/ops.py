@@ -406,3 +406,12 @@ class PreparedQuantize:
         rc = self.lib.qz_quantize(_P(w.data_ptr()), b, r, c, ld_r, ld_b, *self._args_tail, st)
         if rc:
             _lib.check(rc, "qz_quantize")
+
+
+def unpack_zero_points(packed: torch.Tensor, num_bits: int, shape) -> torch.Tensor:
+    """Inverse of pack_to_int32(zp, packed_dim=0): int32 [ceil(R*bits/32), C] -> int8 [R, C]."""
+    pf = 32 // num_bits
+    shifts = torch.arange(pf, device=packed.device, dtype=torch.int32).view(1, -1, 1) * num_bits
+    u = (packed.unsqueeze(1) >> shifts) & ((1 << num_bits) - 1)
+    u = u.reshape(-1, packed.shape[-1])[: int(shape[0])]
+    return (u - (1 << (num_bits - 1))).to(torch.int8)

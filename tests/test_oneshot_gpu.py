@@ -1,0 +1,204 @@
+"""End-to-end on the GPU: oneshot (RTN + AWQ) on small random-weight Qwen3 / Qwen3-MoE models,
+save_compressed -> compressed-tensors checkpoint, bit-exact against the CPU oracle applied to the
+same (smoothed) weights; AWQ checked against an oracle restatement of the search."""
+import json
+import os
+
+import pytest
+import torch
+
+import ct_torch as ct
+from quantizers_amd import ops
+from quantizers_amd.awq import DEFAULT_MAPPINGS, resolve_mappings
+from quantizers_amd.compressor import compressed_state_dict, load_decompressed, save_compressed
+from quantizers_amd.oneshot import oneshot
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _qwen3(layers=2, hidden=256, inter=512):
+    from transformers import AutoModelForCausalLM, Qwen3Config
+    cfg = Qwen3Config(hidden_size=hidden, intermediate_size=inter, num_hidden_layers=layers, num_attention_heads=4,
+                      num_key_value_heads=2, head_dim=64, vocab_size=512, max_position_embeddings=256)
+    torch.manual_seed(0)
+    m = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    with torch.no_grad():  # non-trivial norms so smoothing has something to move
+        for n, p in m.named_parameters():
+            if n.endswith("layernorm.weight"):
+                p.copy_((torch.rand_like(p.float()) * 1.5 + 0.25).to(p.dtype))
+    return m
+
+
+def _qwen3_moe():
+    from transformers import AutoModelForCausalLM, Qwen3MoeConfig
+    cfg = Qwen3MoeConfig(hidden_size=128, intermediate_size=256, moe_intermediate_size=64, num_hidden_layers=2,
+                         num_attention_heads=4, num_key_value_heads=2, head_dim=32, vocab_size=256, num_experts=8,
+                         num_experts_per_tok=2)
+    torch.manual_seed(0)
+    return AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+
+
+def _calib(n=4, s=64, vocab=512):
+    g = torch.Generator().manual_seed(42)
+    return [{"input_ids": torch.randint(0, vocab, (s,), generator=g)} for _ in range(n)]
+
+
+def _oa(a):
+    sd = {None: None, "float8_e4m3fn": "fp8", "uint8": "e8m0"}[a.scale_dtype]
+    return ct.QArgs(num_bits=a.num_bits, type=a.type, symmetric=a.symmetric, strategy=a.strategy,
+                    group_size=a.group_size, block_structure=tuple(a.block_structure) if a.block_structure else None,
+                    scale_dtype=sd)
+
+
+def _eq(a, b, key=""):
+    a, b = a.cpu(), b.cpu()
+    assert a.shape == b.shape, (key, a.shape, b.shape)
+    if a.dtype in (torch.bfloat16, torch.float8_e4m3fn):
+        a = a.view(torch.int16 if a.dtype == torch.bfloat16 else torch.uint8)
+        b = b.view(torch.int16 if b.dtype == torch.bfloat16 else torch.uint8)
+    assert torch.equal(a, b), key
+
+
+def _check_against_oracle(model, sd):
+    """Every targeted module's on-disk tensors == oracle compress of its current bf16 weight."""
+    from quantizers_amd.model import iter_linears
+    n = 0
+    for ref in iter_linears(model):
+        sch = model.quantization_scheme_map.get(ref.name)
+        if sch is None:
+            assert f"{ref.name}.weight" in sd
+            continue
+        want = ct.compress_weight(ref.weight.detach().cpu().contiguous(), _oa(sch.weights))
+        for k, v in want.items():
+            _eq(sd[f"{ref.name}.{k}"], v, f"{ref.name}.{k}")
+        n += 1
+    return n
+
+
+def test_rtn_w4a16_save_roundtrip(cuda, tmp_path):
+    m = _qwen3().to(cuda)
+    recipe = {"s": {"m": {"QuantizationModifier": {"scheme": "W4A16", "targets": "Linear", "ignore": ["lm_head"]}}}}
+    oneshot(m, recipe)
+    out = save_compressed(m, str(tmp_path / "w4a16"))
+    cfg = json.load(open(os.path.join(out, "config.json")))["quantization_config"]
+    assert cfg["quant_method"] == "compressed-tensors" and cfg["format"] == "pack-quantized"
+    assert cfg["quantization_status"] == "compressed" and cfg["ignore"] == ["lm_head"]
+    g = cfg["config_groups"]["group_0"]["weights"]
+    assert (g["num_bits"], g["group_size"], g["strategy"], g["symmetric"]) == (4, 128, "group", True)
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 14
+    # decompress and compare with the oracle fake-quant
+    dec = load_decompressed(out)
+    w = m.model.layers[0].mlp.down_proj.weight.detach().cpu()
+    oa = ct.QArgs(num_bits=4, group_size=128)
+    mn, mx = ct.observe_minmax(w, oa)
+    s, z = ct.calculate_qparams(mn, mx, oa)
+    q = ct.quantize(w, s, z, oa, dtype=torch.int8)
+    _eq(dec["model.layers.0.mlp.down_proj.weight"], ct.dequantize(q, s, None, oa, dtype=torch.bfloat16))
+
+
+def test_awq_int4_g32_end_to_end(cuda, tmp_path):
+    torch.manual_seed(0)
+    m = _qwen3().to(cuda)
+    calib = _calib()
+    ids = torch.stack([c["input_ids"] for c in calib]).to(cuda)
+    with torch.no_grad():
+        ref_logits = m(ids).logits.float()
+    recipe = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g32.yaml")
+    oneshot(m, recipe, dataset=calib, max_seq_length=64)
+    rep = m.awq_report
+    assert len(rep) == 2
+    for layer, maps in rep.items():
+        # v_proj -> o_proj skipped for GQA (D9): 3 mappings per layer
+        assert len(maps) == 3, maps.keys()
+        for smooth, r in maps.items():
+            assert 0.0 <= r["best_ratio"] < 1.0 and len(r["history"]) == 20
+            assert r["best_loss"] <= r["history"][0] + 1e-12
+    # smoothing preserves the function (up to bf16 rounding of the rescaled weights)
+    with torch.no_grad():
+        new_logits = m(ids).logits.float()
+    rel = (new_logits - ref_logits).norm() / ref_logits.norm()
+    assert rel < 0.05, rel
+    out = save_compressed(m, str(tmp_path / "awq"))
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 14
+    assert os.path.exists(os.path.join(out, "model.safetensors"))
+
+
+def test_awq_layer_matches_oracle_search(cuda):
+    """Layer-0 AWQ: statistics, w_mean and grid losses from the GPU path vs a CPU restatement."""
+    from quantizers_amd.quantization import QuantizationArgs
+    m = _qwen3(layers=1).to(cuda)
+    calib = _calib(n=2, s=32)
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    layer = m.model.layers[0]
+    names = [f"model.layers.0.mlp.{p}" for p in ("gate_proj", "up_proj", "down_proj")]
+    quantized = {n: a for n in names}
+    (r,) = [x for x in resolve_mappings(layer, "model.layers.0", DEFAULT_MAPPINGS, quantized)
+            if x.smooth_name.endswith("post_attention_layernorm")]
+    # inputs of the MLP for each sample
+    xs = []
+    h = layer.mlp.register_forward_pre_hook(lambda mod, args: xs.append(args[0].detach().clone()))
+    with torch.no_grad():
+        for c in calib:
+            m(c["input_ids"].unsqueeze(0).to(cuda))
+    h.remove()
+    gw, uw = layer.mlp.gate_proj.weight.detach(), layer.mlp.up_proj.weight.detach()
+    # GPU statistics
+    sums = torch.zeros(gw.shape[1], dtype=torch.float32, device=cuda)
+    cnt = sum(ops.awq_absmean_accum(x, sums) for x in xs)
+    x_mean = sums / cnt
+    wsum = torch.zeros(gw.shape[1], dtype=torch.float64, device=cuda)
+    rows = ops.awq_weight_mean_accum(gw, 32, wsum) + ops.awq_weight_mean_accum(uw, 32, wsum)
+    w_mean = wsum / rows
+    # CPU restatement
+    xc = [x.cpu() for x in xs]
+    s_ref, n_ref = None, 0
+    for x in xc:
+        s_ref = ct.awq_accumulate_mean(x, None if s_ref is None else (s_ref, n_ref))
+        s_ref, n_ref = s_ref
+    torch.testing.assert_close(x_mean.cpu(), s_ref / n_ref, rtol=1e-5, atol=1e-6)
+    wm_ref = ct.awq_layer_means([gw.cpu(), uw.cpu()], ct.QArgs(group_size=32))
+    torch.testing.assert_close(w_mean.cpu(), wm_ref, rtol=1e-12, atol=1e-12)
+    # grid: GPU losses vs CPU losses for the same scales (parent = mlp)
+    mlp_cpu = layer.mlp.to("cpu").float()
+    mlp_gpu = layer.mlp.to(cuda)
+    ref_out = [mlp_gpu(x).float() for x in xs]
+    for ratio in (0.0, 0.45, 0.9):
+        s = ops.awq_grid_scales(x_mean, w_mean.float(), ratio, True)
+        s_c = ct.awq_grid_scales(s_ref / n_ref, wm_ref, ratio, True)
+        torch.testing.assert_close(s.cpu(), s_c, rtol=1e-5, atol=1e-7)
+        g_fq = ops.fake_quantize(gw, a, col_scales=s)
+        g_ref = ct.awq_fake_quant_scaled(gw.cpu(), s.cpu(), ct.QArgs(group_size=32))
+        _eq(g_fq, g_ref, f"fake-quant ratio {ratio}")
+    mlp_cpu.to(torch.bfloat16)
+
+
+def test_mixed_fp8_block_and_awq(cuda, tmp_path):
+    m = _qwen3().to(cuda)
+    oneshot(m, os.path.join(ROOT, "configs/recipes/mixed_fp8_block_awq_int4.yaml"), dataset=_calib(),
+            max_seq_length=64)
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 14
+    assert sd["model.layers.0.self_attn.q_proj.weight"].dtype == torch.float8_e4m3fn
+    assert sd["model.layers.0.self_attn.q_proj.weight_scale"].shape == (2, 2)
+    save_compressed(m, str(tmp_path / "mixed"))
+    cfg = json.load(open(tmp_path / "mixed" / "config.json"))["quantization_config"]
+    assert cfg["format"] == "mixed-precision"
+    assert {g["format"] for g in cfg["config_groups"].values()} == {"float-quantized", "pack-quantized"}
+
+
+@pytest.mark.parametrize("recipe,key", [("moe_experts_nvfp4.yaml", "weight_global_scale"),
+                                        ("moe_experts_mxfp4.yaml", "weight_packed")])
+def test_moe_fused_experts(cuda, tmp_path, recipe, key):
+    m = _qwen3_moe().to(cuda)
+    oneshot(m, os.path.join(ROOT, "configs/recipes", recipe))
+    names = sorted(m.quantization_scheme_map)
+    assert len(names) == 2 * 8 * 3  # layers x experts x {gate, up, down}
+    assert "model.layers.1.mlp.experts.7.down_proj" in names
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 48
+    assert f"model.layers.0.mlp.experts.3.gate_proj.{key}" in sd
+    assert not any(k.endswith("experts.gate_up_proj") for k in sd)
+    save_compressed(m, str(tmp_path / "moe"))

@@ -246,3 +246,20 @@ def test_smoothing_ops(cuda):
     n = _w(1, 128, seed=4).reshape(-1)
     got = ops.scale_rows_(n.clone().to(cuda), s.to(cuda), divide=True)
     _eq(got, (n.float() / s).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("scheme", [SCHEMES[1], SCHEMES[17], SCHEMES[18], SCHEMES[11]], ids=_id)
+def test_fused_expert_strided_slices(cuda, scheme):
+    """[E, 2I, H] fused gate_up parameter: the gate half [:, :I] is a strided batch view."""
+    a = QuantizationArgs(**scheme)
+    g = torch.Generator().manual_seed(3)
+    fused = (torch.randn(6, 2 * 64, 128, generator=g) * 0.02).to(torch.bfloat16)
+    view = fused.to(cuda)[:, :64, :]
+    got = ops.compress_weight(view, a)
+    for e in range(6):
+        ref = ct.compress_weight(fused[e, :64].contiguous(), _oracle_args(a))
+        for k, v in ref.items():
+            if k == "weight_shape":
+                continue
+            gv = got[k][e] if got[k].dim() > 1 or k != "weight_global_scale" else got[k][e:e + 1]
+            _eq(gv, v)
