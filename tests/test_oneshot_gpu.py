@@ -161,10 +161,7 @@ def test_awq_layer_matches_oracle_search(cuda):
     torch.testing.assert_close(x_mean.cpu(), s_ref / n_ref, rtol=1e-5, atol=1e-6)
     wm_ref = ct.awq_layer_means([gw.cpu(), uw.cpu()], ct.QArgs(group_size=32))
     torch.testing.assert_close(w_mean.cpu(), wm_ref, rtol=1e-12, atol=1e-12)
-    # grid: GPU losses vs CPU losses for the same scales (parent = mlp)
-    mlp_cpu = layer.mlp.to("cpu").float()
-    mlp_gpu = layer.mlp.to(cuda)
-    ref_out = [mlp_gpu(x).float() for x in xs]
+    # grid points: scale vectors and the fused Q(W*s)/s step vs the restatement
     for ratio in (0.0, 0.45, 0.9):
         s = ops.awq_grid_scales(x_mean, w_mean.float(), ratio, True)
         s_c = ct.awq_grid_scales(s_ref / n_ref, wm_ref, ratio, True)
@@ -172,7 +169,6 @@ def test_awq_layer_matches_oracle_search(cuda):
         g_fq = ops.fake_quantize(gw, a, col_scales=s)
         g_ref = ct.awq_fake_quant_scaled(gw.cpu(), s.cpu(), ct.QArgs(group_size=32))
         _eq(g_fq, g_ref, f"fake-quant ratio {ratio}")
-    mlp_cpu.to(torch.bfloat16)
 
 
 def test_mixed_fp8_block_and_awq(cuda, tmp_path):
