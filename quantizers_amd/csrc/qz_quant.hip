@@ -102,11 +102,8 @@ struct FastArgs {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef QZ_NT_LOADS
-#define QZ_NT_LOADS 0
-#endif
-#ifndef QZ_NT_STORES
-#define QZ_NT_STORES 0
+#ifndef QZ_LDS_AUX
+#define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
 
 // round both lanes of an f32 pair to bf16 (one v_cvt_pk_bf16_f32) and widen back
@@ -119,7 +116,7 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
 }
 
 // Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
-template <int LOGL, int KIND, bool FQ>
+template <int LOGL, int KIND, bool FQ, bool SYM>
 __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
                                              const bool valid, const float gs, const int lane) {
   constexpr int L = 1 << LOGL;
@@ -144,7 +141,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
 
   // ---- observe: memoryless min/max over the group (exact in bf16), on integer keys
   float mn, mx;
-  if (p.sym) {
+  if (SYM) {
     uint32_t am;
     if (FQ && A.col_scales) {
       am = 0;
@@ -170,7 +167,9 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
     mn = key2f(grp_min_u<L>(kmn));
     mx = key2f(grp_max_u<L>(kmx));
   }
-  const GP g = group_params(p, mn, mx, gs);
+  QP ps = p;
+  ps.sym = SYM;
+  const GP g = group_params(ps, mn, mx, gs);
 
   // ---- quotient x / scale (bf16; f32 for NVFP4); x * rcp(s) is exact-equivalent (rcp lemma)
   f32x2 t[4];
@@ -198,7 +197,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x2 tk = t[k];
-      if (!p.sym) tk = bfr2(tk + zp2);
+      if (!SYM) tk = bfr2(tk + zp2);
       tk.x = __builtin_amdgcn_fmed3f(tk.x, p.qmin, p.qmax);
       tk.y = __builtin_amdgcn_fmed3f(tk.y, p.qmin, p.qmax);
       t[k] = tk;
@@ -284,22 +283,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
 }
 
-// branch-free: out-of-range lanes re-load the slice's last unit (results never stored)
-__device__ __forceinline__ void load_tile(const FastArgs& A, const uint16_t* wb, int64_t tile, int lane, uint4* v) {
-#pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
-    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
-#if QZ_NT_LOADS
-    const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wb) + unit);
-    v[u] = make_uint4(t.x, t.y, t.z, t.w);
-#else
-    v[u] = reinterpret_cast<const uint4*>(wb)[unit];
-#endif
-  }
-}
-
-template <int LOGL, int KIND, bool FQ>
+template <int LOGL, int KIND, bool FQ, bool SYM>
 __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t b, int64_t tile,
                                              int lane) {
   const float gs = (KIND == K_NV) ? A.gscale[b] : 0.f;
@@ -315,28 +299,43 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
       if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
     }
 #else
-    process_unit<LOGL, KIND, FQ>(A, p, v[u], unit, valid, gs, lane);
+    process_unit<LOGL, KIND, FQ, SYM>(A, p, v[u], unit, valid, gs, lane);
 #endif
   }
 }
 
-// One tile (UNROLL*64 units = UNROLL KiB of bf16) per wave, all UNROLL 16-B loads issued
-// before any arithmetic; latency is hidden by occupancy (up to 8 waves per SIMD).  Measured
-// on MI355X this beats a persistent grid-stride loop with register double-buffering (the
-// VALU-heavy waves need other resident waves to overlap with, not deeper per-wave queues).
-// grid = (tiles per slice, batch): batch slices may be strided (fused-expert views).
-template <int LOGL, int KIND, bool FQ>
+// One tile (UNROLL*64 units = UNROLL KiB of bf16) per wave.  The tile is streamed HBM -> LDS
+// with global_load_lds_dwordx4 (LDS-DMA: no VGPR destination, 1 KiB per wave-instruction,
+// fully coalesced), the wave waits on its own vmcnt and reads its lanes' 16 B back with
+// ds_read_b128; latency is hidden by occupancy (one-shot waves, up to 8 per SIMD).  Measured on
+// MI355X (scripts/tune_fast.py): LDS-DMA staging is 5 % faster than register loads here, and a
+// persistent grid-stride loop with register double-buffering is slower than one-shot waves.
+// Out-of-range lanes re-load the slice's last unit (results never stored), keeping the
+// loads branch-free.  grid = (tiles per slice, batch): slices may be strided (fused experts).
+template <int LOGL, int KIND, bool FQ, bool SYM>
 __global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
+  __shared__ uint4 lds_buf[BLOCK / WAVE][UNROLL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t tile = (int64_t)blockIdx.x * (BLOCK / WAVE) + (threadIdx.x >> 6);
+  const int w = threadIdx.x >> 6;
+  const int64_t tile = (int64_t)blockIdx.x * (BLOCK / WAVE) + w;
   const int64_t tiles = (A.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
   if (tile >= tiles) return;
   const int64_t b = blockIdx.y;
+  const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
+    __builtin_amdgcn_global_load_lds((const void*)(src + unit),
+                                     (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0, QZ_LDS_AUX);
+  }
   QP p = A.p;
   p.kind = KIND;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
   uint4 v[UNROLL];
-  load_tile(A, A.w + b * A.ld_batch, tile, lane, v);
-  process_tile<LOGL, KIND, FQ>(A, p, v, b, tile, lane);
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
+  process_tile<LOGL, KIND, FQ, SYM>(A, p, v, b, tile, lane);
 }
 
 // ------------------------------------------------------------------ generic path
@@ -555,29 +554,29 @@ __global__ void k_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int bi
 // ---------------------------------------------------------------------- host side
 using FastFn = void (*)(FastArgs);
 
-template <int LOGL, int KIND>
+template <int LOGL, int KIND, bool SYM>
 FastFn pick_fq(bool fq) {
-  return fq ? (FastFn)k_group_fast<LOGL, KIND, true> : (FastFn)k_group_fast<LOGL, KIND, false>;
+  return fq ? (FastFn)k_group_fast<LOGL, KIND, true, SYM> : (FastFn)k_group_fast<LOGL, KIND, false, SYM>;
 }
 template <int LOGL>
-FastFn pick_kind(int kind, bool fq) {
+FastFn pick_kind(int kind, bool sym, bool fq) {
   switch (kind) {
-    case K_INT: return pick_fq<LOGL, K_INT>(fq);
-    case K_FP8: return pick_fq<LOGL, K_FP8>(fq);
-    case K_MX: return pick_fq<LOGL, K_MX>(fq);
-    case K_NV: return pick_fq<LOGL, K_NV>(fq);
-    default: return pick_fq<LOGL, K_FP4>(fq);
+    case K_INT: return sym ? pick_fq<LOGL, K_INT, true>(fq) : pick_fq<LOGL, K_INT, false>(fq);
+    case K_FP8: return pick_fq<LOGL, K_FP8, true>(fq);
+    case K_MX: return pick_fq<LOGL, K_MX, true>(fq);
+    case K_NV: return pick_fq<LOGL, K_NV, true>(fq);
+    default: return pick_fq<LOGL, K_FP4, true>(fq);
   }
 }
-FastFn pick_fast(int logl, int kind, bool fq) {
+FastFn pick_fast(int logl, int kind, bool sym, bool fq) {
   switch (logl) {
-    case 0: return pick_kind<0>(kind, fq);
-    case 1: return pick_kind<1>(kind, fq);
-    case 2: return pick_kind<2>(kind, fq);
-    case 3: return pick_kind<3>(kind, fq);
-    case 4: return pick_kind<4>(kind, fq);
-    case 5: return pick_kind<5>(kind, fq);
-    default: return pick_kind<6>(kind, fq);
+    case 0: return pick_kind<0>(kind, sym, fq);
+    case 1: return pick_kind<1>(kind, sym, fq);
+    case 2: return pick_kind<2>(kind, sym, fq);
+    case 3: return pick_kind<3>(kind, sym, fq);
+    case 4: return pick_kind<4>(kind, sym, fq);
+    case 5: return pick_kind<5>(kind, sym, fq);
+    default: return pick_kind<6>(kind, sym, fq);
   }
 }
 
@@ -807,7 +806,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     while ((8 << logl) < g) ++logl;
     const int64_t n_tiles = cdiv(F.units_per_batch, UNROLL * WAVE);
     const int64_t blocks = cdiv(n_tiles, BLOCK / WAVE);
-    hipLaunchKernelGGL(pick_fast(logl, pl.kind, fq), dim3((unsigned)blocks, (unsigned)batch), dim3(BLOCK), 0, st, F);
+    hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq), dim3((unsigned)blocks, (unsigned)batch), dim3(BLOCK), 0, st, F);
     return launch_err();
   }
 
