@@ -102,6 +102,12 @@ struct FastArgs {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#ifndef QZ_HW_FP8
+#define QZ_HW_FP8 1
+#endif
+#ifndef QZ_HW_FP4
+#define QZ_HW_FP4 1
+#endif
 #ifndef QZ_LDS_AUX
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
@@ -249,8 +255,24 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (KIND == K_FP8) {
+#if QZ_HW_FP8  // v_cvt_pk_fp8_f32 (OCP e4m3, RNE); exhaustively checked vs torch's cast
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f),
+                                                                      __builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f), 0, false);
+        c[2 * k] = pk & 0xffu;
+        c[2 * k + 1] = (pk >> 8) & 0xffu;
+#else
         c[2 * k] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f)));
         c[2 * k + 1] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f)));
+#endif
+      } else if (QZ_HW_FP4) {
+        // v_cvt_scalef32_pk_fp4_f32: RNE on the E2M1 grid == cast_to_fp4's thresholds (checked
+        // exhaustively); "+ 0" maps an exact -0 input to +0 (torch.sign(-0.) is 0 -> code 0),
+        // small negatives still round to -0 (code 8) as sign(x)*|q| does
+        const uint32_t pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(
+            0u, __builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f) + 0.0f, __builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f) + 0.0f,
+            1.0f, 0);
+        c[2 * k] = pk & 0xfu;
+        c[2 * k + 1] = (pk >> 4) & 0xfu;
       } else {
         c[2 * k] = fp4_code(__builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f));
         c[2 * k + 1] = fp4_code(__builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f));

@@ -263,3 +263,42 @@ def test_fused_expert_strided_slices(cuda, scheme):
                 continue
             gv = got[k][e] if got[k].dim() > 1 or k != "weight_global_scale" else got[k][e:e + 1]
             _eq(gv, v)
+
+
+def _all_bf16(limit):
+    bits = torch.arange(0, 65536, dtype=torch.int32)
+    bits = torch.where(bits >= 32768, bits - 65536, bits).to(torch.int16)
+    x = bits.view(torch.bfloat16)
+    keep = torch.isfinite(x.float()) & (x.float().abs() <= limit)
+    return x[keep]
+
+
+def _rows_with_anchor(vals, anchor, width):
+    """rows of `width` = [anchor, 511 values...] so every group's scale is fixed by the anchor."""
+    per = width - 1
+    n = (vals.numel() + per - 1) // per
+    pad = torch.zeros(n * per - vals.numel(), dtype=torch.bfloat16)
+    body = torch.cat([vals, pad]).reshape(n, per)
+    return torch.cat([torch.full((n, 1), anchor, dtype=torch.bfloat16), body], dim=1)
+
+
+def test_fp8_encode_exhaustive_fast_path(cuda):
+    """Every finite bf16 with |x| <= 448 through the single-pass FP8 kernel with scale 1."""
+    w = _rows_with_anchor(_all_bf16(448.0), 448.0, 512)
+    a = QuantizationArgs(num_bits=8, type="float", group_size=512)
+    got = ops.compress_weight(w.to(cuda), a)
+    assert torch.all(got["weight_scale"].cpu().float() == 1.0)
+    ref = torch.clamp(w, -448, 448).to(torch.float8_e4m3fn)
+    _eq(got["weight"], ref)
+
+
+@pytest.mark.parametrize("anchor", [4.0, 5.96875])
+def test_mxfp4_encode_exhaustive_fast_path(cuda, anchor):
+    """Every finite bf16 with |x| <= anchor through the MXFP4 kernel with E8M0 scale 2^0."""
+    vals = _all_bf16(anchor)
+    w = _rows_with_anchor(vals, anchor, 32)
+    a = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
+    got = ops.compress_weight(w.to(cuda), a)
+    assert torch.all(got["weight_scale"].cpu() == 127)
+    ref = ct.compress_weight(w, _oracle_args(a))
+    _eq(got["weight_packed"], ref["weight_packed"])
