@@ -91,6 +91,54 @@ def cpu_baseline(seconds: float):
                       f"torch threads={threads}, os.cpu_count()={os.cpu_count()}, cpu='{cpu_model()}'"}
 
 
+def _timed(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def other_configs(ops, QuantizationArgs, dev, gen):
+    """BASELINE.json configs[2] (Qwen3-4B FP8_BLOCK attention + int4-g32 MLP) and configs[3]
+    (Qwen3-30B-A3B experts -> MXFP4): one quantize pass over every targeted weight."""
+    res = {}
+    fp8b = QuantizationArgs(num_bits=8, type="float", strategy="block", block_structure=[128, 128])
+    i4 = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    ws = [(fp8b if n.endswith(("q_proj", "k_proj", "v_proj", "o_proj")) else i4,
+           (torch.randn(QWEN3_LAYERS, r, c, device=dev, generator=gen) * 0.02).to(torch.bfloat16))
+          for n, r, c in QWEN3_4B]
+    npar = sum(w.numel() for _, w in ws)
+    t = _timed(lambda: [ops.quantize_weight(w, a) for a, w in ws])
+    res["qwen3_4b_mixed_fp8block_int4g32"] = {"params": npar, "ms": t * 1e3, "params_per_s": npar / t}
+    del ws
+    torch.cuda.empty_cache()
+    # Qwen3-30B-A3B: 48 layers x 128 experts x {gate, up [768, 2048], down [2048, 768]}; 4 resident
+    # layers (fused [E, 2I, H] / [E, H, I] parameters, gate/up as strided views) rotated over 48
+    mx = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
+    layers = []
+    for _ in range(4):
+        gu = (torch.randn(128, 2 * 768, 2048, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+        dn = (torch.randn(128, 2048, 768, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+        layers.append((gu, dn))
+
+    def moe_pass():
+        for li in range(48):
+            gu, dn = layers[li % 4]
+            ops.quantize_weight(gu[:, :768], mx)
+            ops.quantize_weight(gu[:, 768:], mx)
+            ops.quantize_weight(dn, mx)
+    npar = 48 * 128 * 3 * 768 * 2048
+    t = _timed(moe_pass, reps=2)
+    res["qwen3_30b_a3b_experts_mxfp4"] = {"params": npar, "ms": t * 1e3, "params_per_s": npar / t,
+                                          "alg_GBps": npar * (2 + 0.5 + 1 / 32) / t / 1e9}
+    del layers
+    torch.cuda.empty_cache()
+    return res
+
+
 def read_pmc_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -214,6 +262,11 @@ def main():
         model_pass = {"params": nparams, "ms": mp * 1e3, "params_per_s": nparams / mp,
                       "alg_GBps": nparams * (2 + BITS / 8 + 2 / GROUP) / mp / 1e9, "launches": len(ws)}
 
+    # ---- the other BASELINE configs, one whole-model pass each (reported beside the headline)
+    other = None
+    if not args.no_model_pass:
+        other = other_configs(ops, QuantizationArgs, dev, gen)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
@@ -249,6 +302,7 @@ def main():
             "parity_check": ok,
             "allgather_ms": allgather,
             "qwen3_4b_all_linears": model_pass,
+            "other_configs": other,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

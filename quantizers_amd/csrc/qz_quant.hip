@@ -121,61 +121,11 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
   return r;
 }
 
-// Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
-template <int LOGL, int KIND, bool FQ, bool SYM>
-__device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
-                                             const bool valid, const float gs, const int lane) {
-  constexpr int L = 1 << LOGL;
-  // unit: dense output index (batch*units_per_batch + local); valid is uniform within a group
-  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-  f32x2 x[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    x[k].x = __uint_as_float(wd[k] << 16);
-    x[k].y = __uint_as_float(wd[k] & 0xffff0000u);
-  }
-  f32x2 cs[4];
-  if (FQ && A.col_scales) {
-    const int64_t c0 = (unit % A.units_per_row) * 8;
-    const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
-    const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
-    cs[0] = f32x2{c_lo.x, c_lo.y}; cs[1] = f32x2{c_lo.z, c_lo.w};
-    cs[2] = f32x2{c_hi.x, c_hi.y}; cs[3] = f32x2{c_hi.z, c_hi.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = bfr2(x[k] * cs[k]);  // W * s in the weight dtype
-  }
-
-  // ---- observe: memoryless min/max over the group (exact in bf16), on integer keys
-  float mn, mx;
-  if (SYM) {
-    uint32_t am;
-    if (FQ && A.col_scales) {
-      am = 0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        am = max(am, max(__float_as_uint(x[k].x) & 0x7fffffffu, __float_as_uint(x[k].y) & 0x7fffffffu));
-    } else {  // |bf16| bit patterns, two per dword: v_pk_max_u16 on the raw words
-      const uint32_t m = pk_max_u16(pk_max_u16(wd[0] & 0x7fff7fffu, wd[1] & 0x7fff7fffu),
-                                    pk_max_u16(wd[2] & 0x7fff7fffu, wd[3] & 0x7fff7fffu));
-      am = max(m & 0xffffu, m >> 16) << 16;
-    }
-    am = grp_max_u<L>(am);
-    mx = __uint_as_float(am);
-    mn = -mx;
-  } else {
-    uint32_t kmn = 0xffffffffu, kmx = 0u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t a = f2key(x[k].x), b = f2key(x[k].y);
-      kmn = min(kmn, min(a, b));
-      kmx = max(kmx, max(a, b));
-    }
-    mn = key2f(grp_min_u<L>(kmn));
-    mx = key2f(grp_max_u<L>(kmx));
-  }
-  QP ps = p;
-  ps.sym = SYM;
-  const GP g = group_params(ps, mn, mx, gs);
+// quotient, round/clamp/encode and store of one 8-element unit whose group params are known.
+// unit = dense output unit index.  Returns false for invalid (out-of-range) units.
+template <int KIND, bool FQ, bool SYM>
+__device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, const GP& g, const f32x2* x,
+                                             const f32x2* cs, const int64_t unit) {
 
   // ---- quotient x / scale (bf16; f32 for NVFP4); x * rcp(s) is exact-equivalent (rcp lemma)
   f32x2 t[4];
@@ -193,7 +143,6 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) t[k] = bfr2(t[k]);
   }
-  if (!valid) return;
 
   if (KIND == K_INT) {
     // clamp (bf16 bounds), then t + (2^23 - qmin): RNE(t) - qmin lands in the low mantissa bits
@@ -297,6 +246,65 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
       reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
     }
   }
+}
+
+// Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
+template <int LOGL, int KIND, bool FQ, bool SYM>
+__device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
+                                             const bool valid, const float gs, const int lane) {
+  constexpr int L = 1 << LOGL;
+  // unit: dense output index (batch*units_per_batch + local); valid is uniform within a group
+  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+  f32x2 x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[k].x = __uint_as_float(wd[k] << 16);
+    x[k].y = __uint_as_float(wd[k] & 0xffff0000u);
+  }
+  f32x2 cs[4];
+  if (FQ && A.col_scales) {
+    const int64_t c0 = (unit % A.units_per_row) * 8;
+    const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
+    const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
+    cs[0] = f32x2{c_lo.x, c_lo.y}; cs[1] = f32x2{c_lo.z, c_lo.w};
+    cs[2] = f32x2{c_hi.x, c_hi.y}; cs[3] = f32x2{c_hi.z, c_hi.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = bfr2(x[k] * cs[k]);  // W * s in the weight dtype
+  }
+
+  // ---- observe: memoryless min/max over the group (exact in bf16), on integer keys
+  float mn, mx;
+  if (SYM) {
+    uint32_t am;
+    if (FQ && A.col_scales) {
+      am = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        am = max(am, max(__float_as_uint(x[k].x) & 0x7fffffffu, __float_as_uint(x[k].y) & 0x7fffffffu));
+    } else {  // |bf16| bit patterns, two per dword: v_pk_max_u16 on the raw words
+      const uint32_t m = pk_max_u16(pk_max_u16(wd[0] & 0x7fff7fffu, wd[1] & 0x7fff7fffu),
+                                    pk_max_u16(wd[2] & 0x7fff7fffu, wd[3] & 0x7fff7fffu));
+      am = max(m & 0xffffu, m >> 16) << 16;
+    }
+    am = grp_max_u<L>(am);
+    mx = __uint_as_float(am);
+    mn = -mx;
+  } else {
+    uint32_t kmn = 0xffffffffu, kmx = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a = f2key(x[k].x), b = f2key(x[k].y);
+      kmn = min(kmn, min(a, b));
+      kmx = max(kmx, max(a, b));
+    }
+    mn = key2f(grp_min_u<L>(kmn));
+    mx = key2f(grp_max_u<L>(kmx));
+  }
+  QP ps = p;
+  ps.sym = SYM;
+  const GP g = group_params(ps, mn, mx, gs);
+  if (!valid) return;
+  encode_store<KIND, FQ, SYM>(A, ps, g, x, cs, unit);
   if ((lane & (L - 1)) == 0) {
     const int64_t gi = unit >> LOGL;
     if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
@@ -358,6 +366,87 @@ __global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
   process_tile<LOGL, KIND, FQ, SYM>(A, p, v, b, tile, lane);
+}
+
+// --------------------------------------------------------------- single-pass tile path
+// One workgroup per quantization group that is too large (or too 2-D) for a lane group: a
+// BLOCK tile (e.g. FP8_BLOCK 128x128), a CHANNEL row, or a group wider than 512.  The tile
+// (<= 256 threads x MAXU units of 8 bf16) is held in registers, min/max reduce across the
+// workgroup (DPP within the wave, LDS across the 4 waves), then every unit is encoded from
+// registers: one HBM read, like the group path.
+struct TileArgs {
+  int64_t rows, tile_rows, tile_w8, tiles_c, ld_row;  // tile_w8 = tile width in units
+};
+
+template <int KIND, bool SYM, int MAXU>
+__global__ __launch_bounds__(BLOCK) void k_tile_fast(FastArgs A, TileArgs T) {
+  __shared__ uint32_t red[2][BLOCK / WAVE];
+  const int64_t b = blockIdx.y;
+  const int64_t tid = blockIdx.x;
+  const int64_t tr = tid / T.tiles_c, tc = tid % T.tiles_c;
+  const uint32_t U = (uint32_t)(T.tile_rows * T.tile_w8);
+  const uint16_t* wb = A.w + b * A.ld_batch;
+  uint4 v[MAXU];
+  int64_t oidx[MAXU];
+#pragma unroll
+  for (int i = 0; i < MAXU; ++i) {
+    const uint32_t u = threadIdx.x + i * BLOCK;
+    const uint32_t uu = u < U ? u : U - 1;
+    const int64_t row = tr * T.tile_rows + uu / (uint32_t)T.tile_w8;
+    const int64_t c8 = tc * T.tile_w8 + uu % (uint32_t)T.tile_w8;
+    v[i] = *reinterpret_cast<const uint4*>(wb + row * T.ld_row + c8 * 8);
+    oidx[i] = (u < U) ? (b * T.rows + row) * A.units_per_row + c8 : -1;
+  }
+  QP p = A.p;
+  p.kind = KIND;
+  p.sym = SYM;
+  // per-thread then workgroup min/max on integer keys
+  uint32_t kmn = 0xffffffffu, kmx = 0u;
+#pragma unroll
+  for (int i = 0; i < MAXU; ++i) {
+    if (oidx[i] < 0) continue;
+    const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float lo = __uint_as_float(wd[k] << 16), hi = __uint_as_float(wd[k] & 0xffff0000u);
+      if (SYM) {
+        kmx = max(kmx, max(__float_as_uint(lo) & 0x7fffffffu, __float_as_uint(hi) & 0x7fffffffu));
+      } else {
+        const uint32_t ka = f2key(lo), kb = f2key(hi);
+        kmn = min(kmn, min(ka, kb));
+        kmx = max(kmx, max(ka, kb));
+      }
+    }
+  }
+  kmx = grp_max_u<WAVE>(kmx);
+  if (!SYM) kmn = grp_min_u<WAVE>(kmn);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[0][w] = kmn; red[1][w] = kmx; }
+  __syncthreads();
+  kmn = red[0][0];
+  kmx = red[1][0];
+#pragma unroll
+  for (int k = 1; k < BLOCK / WAVE; ++k) { kmn = min(kmn, red[0][k]); kmx = max(kmx, red[1][k]); }
+  float mn, mx;
+  if (SYM) { mx = __uint_as_float(kmx); mn = -mx; }
+  else { mn = key2f(kmn); mx = key2f(kmx); }
+  const GP g = group_params(p, mn, mx, 0.f);
+  f32x2 cs[4];
+#pragma unroll
+  for (int i = 0; i < MAXU; ++i) {
+    if (oidx[i] < 0) continue;
+    const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+    f32x2 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { x[k].x = __uint_as_float(wd[k] << 16); x[k].y = __uint_as_float(wd[k] & 0xffff0000u); }
+    encode_store<KIND, false, SYM>(A, p, g, x, cs, oidx[i]);
+  }
+  if (threadIdx.x == 0) {
+    const int64_t gi = b * (int64_t)gridDim.x + tid;
+    if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
+    else reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
+    if (A.zp_out) A.zp_out[gi] = (int8_t)g.zp;
+  }
 }
 
 // ------------------------------------------------------------------ generic path
@@ -602,6 +691,25 @@ FastFn pick_fast(int logl, int kind, bool sym, bool fq) {
   }
 }
 
+using TileFn = void (*)(FastArgs, TileArgs);
+template <int KIND, bool SYM>
+TileFn pick_tile_u(int maxu) {
+  switch (maxu) {
+    case 1: return k_tile_fast<KIND, SYM, 1>;
+    case 2: return k_tile_fast<KIND, SYM, 2>;
+    case 4: return k_tile_fast<KIND, SYM, 4>;
+    case 8: return k_tile_fast<KIND, SYM, 8>;
+    default: return k_tile_fast<KIND, SYM, 16>;
+  }
+}
+TileFn pick_tile(int kind, bool sym, int maxu) {
+  switch (kind) {
+    case K_INT: return sym ? pick_tile_u<K_INT, true>(maxu) : pick_tile_u<K_INT, false>(maxu);
+    case K_FP8: return pick_tile_u<K_FP8, true>(maxu);
+    default: return pick_tile_u<K_FP4, true>(maxu);
+  }
+}
+
 struct Plan {
   QP p;
   int kind;
@@ -830,6 +938,46 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     const int64_t blocks = cdiv(n_tiles, BLOCK / WAVE);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq), dim3((unsigned)blocks, (unsigned)batch), dim3(BLOCK), 0, st, F);
     return launch_err();
+  }
+
+  // single-pass tile path: BLOCK tiles, CHANNEL rows, wide groups (one workgroup per group)
+  {
+    int64_t th = 0, tw = 0;
+    if (a->strategy == QZ_BLOCK) { th = a->block_h; tw = a->block_w; }
+    else if (a->strategy == QZ_CHANNEL) { th = 1; tw = cols; }
+    else if (grp && g > 0) { th = 1; tw = g; }
+    const int64_t U = th * (tw / 8);
+    const bool kind_ok = pl.kind == K_INT || pl.kind == K_FP8 || pl.kind == K_FP4;
+    const bool row_al = ld_row % 8 == 0 && (batch == 1 || ld_batch % 8 == 0) && cols % 8 == 0;
+    if (!fq && kind_ok && th > 0 && tw % 8 == 0 && U >= 64 && U <= 16 * BLOCK && row_al && pack_ok && al &&
+        batch <= 65535) {
+      FastArgs F;
+      F.w = (const uint16_t*)w;
+      F.n_units = batch * rows * cols / 8;
+      F.units_per_batch = rows * cols / 8;
+      F.units_per_row = cols / 8;
+      F.ld_batch = batch > 1 ? ld_batch : rows * ld_row;
+      F.p = pl.p;
+      F.out_fmt = out_fmt;
+      F.scale_bytes = pl.scale_bytes;
+      F.q_out = q_out;
+      F.s_out = s_dst;
+      F.zp_out = z_dst;
+      F.gscale = gs_dst;
+      F.col_scales = nullptr;
+      TileArgs T;
+      T.rows = rows;
+      T.tile_rows = th;
+      T.tile_w8 = tw / 8;
+      T.tiles_c = cols / tw;
+      T.ld_row = ld_row;
+      const int64_t tiles = (rows / th) * (cols / tw);
+      int maxu = 1;
+      while (maxu * BLOCK < U) maxu *= 2;
+      hipLaunchKernelGGL(pick_tile(pl.kind, pl.p.sym != 0, maxu), dim3((unsigned)tiles, (unsigned)batch), dim3(BLOCK),
+                         0, st, F, T);
+      return launch_err();
+    }
   }
 
   // generic: min/max -> qparams -> quantize
