@@ -16,20 +16,36 @@ configs/recipes/recipe_awq_w4a16.yaml:11-31)
 4. ``_apply_smoothing``: balance W[:, c] *= s[c]; smooth norm w /= s, or a smooth Linear's
    last len(s) output rows (and bias) /= s (``qz_scale_columns`` / ``qz_scale_rows``).
 
-Mappings whose balance in_features differ from the smooth layer's output width are skipped
-(GQA v_proj->o_proj, decision D9).  The parent forwards are PyTorch GEMMs.
+Mapping resolution follows llmcompressor ``_set_resolved_mappings``: every module matching
+``smooth_layer``; its balance layers are all targets under the smooth layer's parent matching
+a ``balance_layers`` regex; a Linear balance whose in_features differ from a Linear smooth
+layer's out_features is dropped (GQA v_proj->o_proj, decision D9); the loss parent is the
+single balance layer, else the lowest common ancestor that is not a ModuleList.
+
+MoE experts (transformers-5 fused ``gate_up_proj`` / ``down_proj`` parameters) are resolved
+under the per-expert names of the reference's transformers 4.57 layout (model.py), so the
+MiniMax recipes' ``post_attention_layernorm -> w1, w3`` (all experts, parent = the MoE block)
+and ``w3 -> w2`` (one expert, parent = that expert's w2) mappings work unchanged
+(recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:49-56).  ``moe_calibrate_all_experts=True`` semantics:
+an expert's linears see every calibration token (the experts module's input), not only the
+tokens routed to it; with False, only the routed tokens (from the router's top-k indices).
+Inputs of a per-expert ``w2`` are recomputed from the cached experts input and a snapshot of
+the pre-smoothing gate/up weights, so nothing of size tokens x experts is kept resident.
+The parent forwards are PyTorch GEMMs; the grid's losses stay on the device (one host sync
+per mapping).
 """
 from __future__ import annotations
 
 import logging
 import re
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 import torch
 from torch import nn
 
 from . import ops
+from .model import LinearRef, batch_groups, checkpoint_name, is_fused_experts, iter_linears, stacked_view
 from .quantization import QuantizationArgs
 from .recipe import AWQMapping
 
@@ -51,11 +67,13 @@ def _rx(t: str) -> str:
 @dataclass
 class ResolvedMapping:
     smooth_name: str
-    smooth: nn.Module
+    smooth: Any                      # norm / Linear module, or a LinearRef (virtual expert linear)
     balance_names: List[str]
-    balance: List[nn.Linear]
+    balance: List[LinearRef]
     parent_name: str
-    parent: nn.Module
+    parent: Optional[nn.Module]      # real module re-run for the loss; None = virtual
+    parent_kind: str = "module"      # "module" | "linear" (one virtual linear) | "expert" (one expert MLP)
+    parent_expert: int = -1
 
 
 def _common_parent(names: List[str]) -> str:
@@ -69,37 +87,62 @@ def _common_parent(names: List[str]) -> str:
     return ".".join(common)
 
 
+def _out_features(m) -> int:
+    return m.weight.shape[0]
+
+
 def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
-                     quantized: Dict[str, QuantizationArgs]) -> List[ResolvedMapping]:
-    """Resolve regex mappings inside one decoder layer (names are relative to the model)."""
-    mods = {f"{prefix}.{n}" if n else prefix: m for n, m in layer.named_modules()}
+                     quantized: Dict[str, QuantizationArgs], mtype: str = "") -> List[ResolvedMapping]:
+    """Resolve regex mappings inside one decoder layer (names are checkpoint names)."""
+    mods = {checkpoint_name(f"{prefix}.{n}" if n else prefix, mtype): m for n, m in layer.named_modules()}
+    lins = {r.name: r for r in iter_linears(layer, prefix, mtype)}
+    virtual = {n: r for n, r in lins.items() if r.index is not None}
     out: List[ResolvedMapping] = []
     for mp in mappings:
         srx = _rx(mp.smooth_layer)
-        smooth_names = [n for n in mods if re.match(srx, n)]
-        for sname in smooth_names:
-            # balance layers: in the same sub-block as the smooth layer (closest matches)
-            balance = []
+        snames = [n for n in mods if re.match(srx, n)] + [n for n in virtual if re.match(srx, n)]
+        for sname in snames:
+            smooth = virtual.get(sname) or mods[sname]
+            sparent = sname.rpartition(".")[0]
+            smooth_is_linear = isinstance(smooth, (nn.Linear, LinearRef))
+            width = smooth.weight.shape[0]
+            balance: List[str] = []
             for brx in mp.balance_layers:
-                cands = [n for n, m in mods.items() if re.match(_rx(brx), n) and isinstance(m, nn.Linear)]
-                if not cands:
-                    continue
-                # pick the candidate sharing the longest prefix with the smooth layer
-                best = max(cands, key=lambda n: len(_common_parent([n, sname])))
-                balance.append(best)
+                for n in lins:
+                    if not n.startswith(sparent + ".") or n in balance:
+                        continue
+                    if not re.match(_rx(brx), n[len(sparent) + 1:]):
+                        continue
+                    if smooth_is_linear and lins[n].weight.shape[1] != width:
+                        log.info("AWQ: dropping balance %s of %s (shape mismatch, D9)", n, sname)
+                        continue
+                    balance.append(n)
             if not balance:
-                continue
-            smod = mods[sname]
-            width = smod.weight.shape[0]
-            lin = [mods[b] for b in balance]
-            if any(l.in_features != width for l in lin):
-                log.info("AWQ: skipping mapping %s -> %s (shape mismatch, D9)", sname, balance)
                 continue
             if not all(b in quantized for b in balance):
                 log.info("AWQ: skipping mapping %s -> %s (balance layers not quantized)", sname, balance)
                 continue
-            pname = balance[0] if len(balance) == 1 else _common_parent(balance)
-            out.append(ResolvedMapping(sname, smod, balance, lin, pname, mods[pname]))
+            refs = [lins[b] for b in balance]
+            if len(balance) == 1:
+                pname = balance[0]
+                if refs[0].index is None:
+                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, refs[0].module))
+                else:
+                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, None, "linear", refs[0].index[0]))
+                continue
+            pname = _common_parent(balance)
+            kind, expert = "module", -1
+            while True:
+                m = mods.get(pname)
+                if m is not None and not isinstance(m, nn.ModuleList) and not is_fused_experts(m):
+                    break
+                if m is None and all(r.index is not None for r in refs) and \
+                        len({(id(r.module), r.index[0]) for r in refs}) == 1 and pname.rpartition(".")[2].isdigit():
+                    kind, expert = "expert", refs[0].index[0]  # one expert's MLP (4.57: experts.<e>)
+                    break
+                pname = pname.rpartition(".")[0]
+            out.append(ResolvedMapping(sname, smooth, balance, refs, pname, mods.get(pname) if kind == "module" else None,
+                                       kind, expert))
     return out
 
 
@@ -120,22 +163,67 @@ class _ParentCache:
 class _AbsMean:
     """Forward pre-hook on a balance layer: sum |x| per input channel (GPU kernel)."""
 
-    def __init__(self, module: nn.Linear):
+    def __init__(self, module: Optional[nn.Module] = None):
         self.sum = None
         self.count = 0
-        self.h = module.register_forward_pre_hook(self._hook)
+        self.h = module.register_forward_pre_hook(self._hook) if module is not None else None
 
     def _hook(self, mod, args):
-        x = args[0]
+        self.add(args[0])
+
+    def add(self, x: torch.Tensor):
         if self.sum is None:
             self.sum = torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device)
-        self.count += ops.awq_absmean_accum(x.detach(), self.sum)
+        if x.numel():
+            self.count += ops.awq_absmean_accum(x.detach(), self.sum)
 
     def mean(self) -> torch.Tensor:
         return self.sum / max(self.count, 1)
 
     def remove(self):
+        if self.h is not None:
+            self.h.remove()
+
+
+class _ExpertInputs:
+    """Inputs of the fused experts module (all tokens + the router's top-k choice) per
+    calibration batch, and per-expert activations recomputed from them on demand."""
+
+    def __init__(self, module: nn.Module, calibrate_all: bool):
+        self.module = module
+        self.calibrate_all = calibrate_all
+        self.x: List[torch.Tensor] = []
+        self.topk: List[Optional[torch.Tensor]] = []
+        self.gate_up0: Optional[torch.Tensor] = None  # pre-smoothing snapshot
+        self.h = module.register_forward_pre_hook(self._hook)
+
+    def _hook(self, mod, args):
+        self.x.append(args[0].detach())
+        self.topk.append(args[1].detach() if len(args) > 1 and torch.is_tensor(args[1]) else None)
+
+    def remove(self):
         self.h.remove()
+
+    def snapshot(self):
+        if self.gate_up0 is None and hasattr(self.module, "gate_up_proj"):
+            self.gate_up0 = self.module.gate_up_proj.data.clone()
+
+    def tokens(self, i: int, e: int) -> torch.Tensor:
+        x = self.x[i]
+        if self.calibrate_all or self.topk[i] is None:
+            return x
+        return x[(self.topk[i] == e).any(dim=-1)]
+
+    def hidden(self, i: int, e: int) -> torch.Tensor:
+        """act(x W_gate^T) * (x W_up^T) for expert e: the input of its down projection."""
+        gate, up = nn.functional.linear(self.tokens(i, e), self.gate_up0[e]).chunk(2, dim=-1)
+        return self.module.act_fn(gate) * up
+
+
+def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
+    if ref.param_name == "down_proj" or ref.param_name == "w2":
+        return ei.hidden(i, ref.index[0])
+    return ei.tokens(i, ref.index[0])
 
 
 def _run_parent(parent: nn.Module, calls) -> List[torch.Tensor]:
@@ -148,13 +236,18 @@ def _run_parent(parent: nn.Module, calls) -> List[torch.Tensor]:
     return outs
 
 
-def _loss(ref: List[torch.Tensor], got: List[torch.Tensor]) -> float:
+def _sq_err(ref: List[torch.Tensor], got: List[torch.Tensor]) -> torch.Tensor:
+    """mean squared error over all calibration outputs, fp64 on the device (no host sync)."""
     tot = torch.zeros((), dtype=torch.float64, device=ref[0].device)
     n = 0
     for a, b in zip(ref, got):
         tot += (a - b).reshape(-1).float().pow(2).sum().double()
         n += a.numel()
-    return (tot / n).item()
+    return tot / max(n, 1)
+
+
+def _loss(ref: List[torch.Tensor], got: List[torch.Tensor]) -> float:
+    return _sq_err(ref, got).item()
 
 
 def _group_size_for_mean(a: QuantizationArgs, cols: int) -> int:
@@ -165,64 +258,138 @@ def _group_size_for_mean(a: QuantizationArgs, cols: int) -> int:
     return cols
 
 
+def _launch_groups(r: ResolvedMapping, quantized: Dict[str, QuantizationArgs]):
+    """Balance refs grouped into single batched launches (same fused parameter, same scheme)."""
+    out = []
+    for g in batch_groups(r.balance):
+        if len(g) > 1 and len({id(quantized[x.name]) for x in g}) > 1:
+            out.extend([[x] for x in g])
+        else:
+            out.append(g)
+    return out
+
+
+def _view(g: List[LinearRef]) -> torch.Tensor:
+    return g[0].weight if len(g) == 1 else stacked_view(g)
+
+
 @torch.no_grad()
 def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dict]], mappings: List[AWQMapping],
-              quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20) -> Dict[str, Any]:
+              quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20,
+              mtype: str = "", calibrate_all_experts: bool = True) -> Dict[str, Any]:
     """Run AWQ on one decoder layer in place.  ``layer_inputs`` are the cached (args, kwargs)
     of the layer for every calibration batch.  Returns per-mapping diagnostics."""
-    resolved = resolve_mappings(layer, prefix, mappings, quantized)
+    resolved = resolve_mappings(layer, prefix, mappings, quantized, mtype)
     if not resolved:
         return {}
-    # 1. one calibration pass: activation statistics + parent inputs
-    stats = {r.smooth_name: _AbsMean(r.balance[0]) for r in resolved}
-    caches = {r.smooth_name: _ParentCache(r.parent) for r in resolved}
+    # 1. one calibration pass: activation statistics + parent inputs (before any smoothing)
+    hooks = []
+    stats: Dict[str, _AbsMean] = {}
+    caches: Dict[str, _ParentCache] = {}
+    experts: Dict[int, _ExpertInputs] = {}
+    for r in resolved:
+        b0 = r.balance[0]
+        if b0.index is None:
+            stats[r.smooth_name] = _AbsMean(b0.module)
+            hooks.append(stats[r.smooth_name])
+        elif id(b0.module) not in experts:
+            experts[id(b0.module)] = _ExpertInputs(b0.module, calibrate_all_experts)
+            hooks.append(experts[id(b0.module)])
+        if r.parent_kind == "module":
+            caches[r.smooth_name] = _ParentCache(r.parent)
+            hooks.append(caches[r.smooth_name])
+        elif id(r.balance[0].module) not in experts:
+            experts[id(r.balance[0].module)] = _ExpertInputs(r.balance[0].module, calibrate_all_experts)
+            hooks.append(experts[id(r.balance[0].module)])
     try:
         for args, kwargs in layer_inputs:
             layer(*args, **kwargs)
     finally:
-        for h in list(stats.values()) + list(caches.values()):
+        for h in hooks:
             h.remove()
+    for ei in experts.values():
+        ei.snapshot()
+    n_batches = len(layer_inputs)
     report = {}
     for r in resolved:
-        x_mean = stats[r.smooth_name].mean()
+        b0 = r.balance[0]
+        if b0.index is None:
+            x_mean = stats[r.smooth_name].mean()
+        else:
+            ei = experts[id(b0.module)]
+            am = _AbsMean()
+            for i in range(n_batches):
+                am.add(_virtual_input(ei, b0, i))
+            if am.count == 0:  # expert never routed to (moe_calibrate_all_experts=False)
+                log.info("AWQ: skipping mapping %s (no calibration tokens)", r.smooth_name)
+                report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "skipped": "no tokens"}
+                continue
+            x_mean = am.mean()
+        groups = _launch_groups(r, quantized)
         # 2. w_mean over the balance layers (each with its own group size)
-        cols = r.balance[0].in_features
+        cols = b0.weight.shape[1]
         wsum = torch.zeros(cols, dtype=torch.float64, device=x_mean.device)
         rows = 0
-        for name, lin in zip(r.balance_names, r.balance):
-            rows += ops.awq_weight_mean_accum(lin.weight.data, _group_size_for_mean(quantized[name], cols), wsum)
+        for g in groups:
+            rows += ops.awq_weight_mean_accum(_view(g), _group_size_for_mean(quantized[g[0].name], cols), wsum)
         w_mean = (wsum / rows).float()
-        calls = caches[r.smooth_name].calls
-        ref_out = _run_parent(r.parent, calls)
-        # 3. grid search
-        orig = [lin.weight.data.clone() for lin in r.balance]
-        best, best_ratio, best_scales, history = float("inf"), -1.0, None, []
+        # parent: forward closure over the calibration batches
+        if r.parent_kind == "module":
+            calls = caches[r.smooth_name].calls
+            run: Callable[[], List[torch.Tensor]] = lambda p=r.parent, c=calls: _run_parent(p, c)
+        else:
+            ei = experts[id(b0.module)]
+            e = r.parent_expert
+            if r.parent_kind == "linear":
+                xin = [_virtual_input(ei, b0, i) for i in range(n_batches)]
+                run = lambda x=xin, ref=b0: [nn.functional.linear(t, ref.weight) for t in x]
+            else:
+                xin = [ei.tokens(i, e) for i in range(n_batches)]
+                mod = b0.module
+
+                def run(x=xin, mod=mod, e=e):
+                    outs = []
+                    for t in x:
+                        gate, up = nn.functional.linear(t, mod.gate_up_proj[e]).chunk(2, dim=-1)
+                        outs.append(nn.functional.linear(mod.act_fn(gate) * up, mod.down_proj[e]))
+                    return outs
+        ref_out = run()
+        # 3. grid search: losses stay on the device
+        orig = [_view(g).clone() for g in groups]
+        tmp = [torch.empty_like(o) for o in orig]
         scales = torch.empty_like(x_mean)
+        losses = []
         for i in range(n_grid):
             ratio = i / n_grid
             ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
-            for name, lin, w0 in zip(r.balance_names, r.balance, orig):
-                ops.fake_quantize(w0, quantized[name], col_scales=scales, out=lin.weight.data)
-            loss = _loss(ref_out, _run_parent(r.parent, calls))
-            history.append(loss)
-            if loss < best:
-                best, best_ratio, best_scales = loss, ratio, scales.clone()
-        for lin, w0 in zip(r.balance, orig):
-            lin.weight.data.copy_(w0)
-        if best_scales is None:
+            for g, w0, t in zip(groups, orig, tmp):
+                if len(g) == 1:
+                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
+                else:
+                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
+                    _view(g).copy_(t)
+            losses.append(_sq_err(ref_out, run()))
+        for g, w0 in zip(groups, orig):
+            _view(g).copy_(w0)
+        history = torch.stack(losses).cpu().tolist()
+        finite = [(l, i) for i, l in enumerate(history) if l == l]
+        if not finite:
             raise RuntimeError(f"AWQ: no finite loss for {r.smooth_name} (history {history})")
+        best, best_i = min(finite)  # first best ratio (strict <): min over (loss, index)
+        best_ratio = best_i / n_grid
+        best_scales = ops.awq_grid_scales(x_mean, w_mean, best_ratio, duo_scaling)
         # 4. apply smoothing
-        for lin in r.balance:
-            ops.scale_columns_(lin.weight.data, best_scales, divide=False)
-        sw = r.smooth.weight.data
+        for g in groups:
+            ops.scale_columns_(_view(g), best_scales, divide=False)
+        sw = r.smooth.weight if isinstance(r.smooth, LinearRef) else r.smooth.weight.data
         if sw.dim() == 1:
             ops.scale_rows_(sw, best_scales, divide=True)
         else:
             ops.scale_rows_(sw[-best_scales.numel():], best_scales, divide=True)
-        b = getattr(r.smooth, "bias", None)
+        b = None if isinstance(r.smooth, LinearRef) else getattr(r.smooth, "bias", None)
         if b is not None:
             ops.scale_rows_(b.data[-best_scales.numel():], best_scales, divide=True)
-        report[r.smooth_name] = {"balance": r.balance_names, "best_ratio": best_ratio, "best_loss": best,
-                                 "history": history}
-        del ref_out
+        report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "best_ratio": best_ratio,
+                                 "best_loss": best, "history": history}
+        del ref_out, orig, tmp
     return report

@@ -21,7 +21,7 @@ from safetensors.torch import load_file, save_file
 from torch import nn
 
 from . import ops
-from .model import batch_groups, iter_linears, stacked_view
+from .model import batch_groups, checkpoint_name, iter_linears, model_type, stacked_view
 from .quantization import QuantizationArgs, QuantizationScheme, compression_format
 
 CT_VERSION = "0.13.1.dev0+quantizers_amd"  # format revision written (reference run: recombine...py:133)
@@ -102,18 +102,21 @@ def compressed_state_dict(model: nn.Module, device=None) -> Dict[str, torch.Tens
                         out[f"{g.name}.{k}"] = v.detach().to("cpu").clone()
                 if r0.index is None and g.bias is not None:
                     out[f"{g.name}.bias"] = g.bias.detach().to("cpu").clone()
+    mtype = model_type(model)
     quant_linears = {g.name for g in refs if g.name in scheme_map and g.index is None}
     for name, prm in model.named_parameters():
         if id(prm) in replaced_params:
             continue
-        mod_name, _, leaf = name.rpartition(".")
+        cname = checkpoint_name(name, mtype)
+        mod_name, _, leaf = cname.rpartition(".")
         if mod_name in quant_linears and leaf in ("weight", "bias"):
             continue
-        if name not in out:
-            out[name] = prm.detach().to("cpu").clone()
+        if cname not in out:
+            out[cname] = prm.detach().to("cpu").clone()
     for name, buf in model.named_buffers():
-        if name not in out and not name.endswith("inv_freq"):
-            out[name] = buf.detach().to("cpu").clone()
+        cname = checkpoint_name(name, mtype)
+        if cname not in out and not name.endswith("inv_freq"):
+            out[cname] = buf.detach().to("cpu").clone()
     return out
 
 

@@ -10,6 +10,8 @@ same-shaped expert slices so the GPU kernel quantizes all experts of a layer in 
 """
 from __future__ import annotations
 
+import re
+
 from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Tuple
 
@@ -62,19 +64,52 @@ def _fused_expert_specs(mod: nn.Module):
     return specs
 
 
-def iter_linears(model: nn.Module) -> List[LinearRef]:
+# transformers-5 runtime names -> the checkpoint names of the transformers version the reference
+# pins (4.57).  Mixtral-family MoE blocks are ``block_sparse_moe`` with experts ``w1`` (gate),
+# ``w3`` (up), ``w2`` (down) on disk (transformers/conversion_mapping.py "mixtral"/"minimax_m2");
+# Qwen-style MoE keeps ``mlp.experts.<e>.{gate,up,down}_proj``.
+MIXTRAL_FAMILY = ("mixtral", "minimax", "minimax_m2")
+
+
+def model_type(model: nn.Module) -> str:
+    return getattr(getattr(model, "config", None), "model_type", "") or ""
+
+
+def checkpoint_name(name: str, mtype: str) -> str:
+    if mtype in MIXTRAL_FAMILY:
+        return re.sub(r"\.mlp(?=\.|$)", ".block_sparse_moe", name)
+    return name
+
+
+def _expert_proj_names(mtype: str):
+    if mtype in MIXTRAL_FAMILY:
+        return {"gate_proj": "w1", "up_proj": "w3", "down_proj": "w2"}
+    return {"gate_proj": "gate_proj", "up_proj": "up_proj", "down_proj": "down_proj"}
+
+
+def iter_linears(model: nn.Module, prefix: str = "", mtype: Optional[str] = None) -> List[LinearRef]:
+    """Every quantization target under ``model`` with its checkpoint name (``prefix`` is
+    prepended for a sub-module such as one decoder layer)."""
+    mtype = model_type(model) if mtype is None else mtype
+    pn = _expert_proj_names(mtype)
     out: List[LinearRef] = []
     for name, mod in model.named_modules():
+        if prefix:
+            name = f"{prefix}.{name}" if name else prefix
         if isinstance(mod, nn.Linear):
-            out.append(LinearRef(name=name, module=mod, param_name="weight", type_name="Linear"))
+            out.append(LinearRef(name=checkpoint_name(name, mtype), module=mod, param_name="weight", type_name="Linear"))
             continue
         for pname, projs in _fused_expert_specs(mod):
             n_exp = getattr(mod, pname).shape[0]
             for e in range(n_exp):
                 for proj, rows in projs:
-                    out.append(LinearRef(name=f"{name}.{e}.{proj}", module=mod, param_name=pname,
-                                         index=(e, rows), type_name="Linear"))
+                    out.append(LinearRef(name=checkpoint_name(f"{name}.{e}.{pn.get(proj, proj)}", mtype), module=mod,
+                                         param_name=pname, index=(e, rows), type_name="Linear"))
     return out
+
+
+def is_fused_experts(mod: nn.Module) -> bool:
+    return bool(_fused_expert_specs(mod))
 
 
 def batch_groups(refs: List[LinearRef]) -> List[List[LinearRef]]:

@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from . import awq as awq_mod
-from .model import LinearRef, decoder_layers, iter_linears
+from .model import LinearRef, checkpoint_name, decoder_layers, iter_linears, model_type
 from .quantization import QuantizationArgs, QuantizationScheme
 from .recipe import AWQModifier, QuantizationModifier, match_any, parse_recipe
 
@@ -102,17 +102,20 @@ def _layer_out(o):
 
 
 @torch.no_grad()
-def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report):
+def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report,
+                    calibrate_all_experts: bool = True):
     layers = decoder_layers(model)
     lname = next(n for n, m in model.named_modules() if m is layers)
     weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
     mappings = awq.mappings or awq_mod.DEFAULT_MAPPINGS
     inputs = _capture_layer0_inputs(model, layers, batches)
+    mtype = model_type(model)
     for i, layer in enumerate(layers):
         home = next(layer.parameters()).device
         layer.to(device)
         t0 = time.time()
-        rep = awq_mod.awq_layer(layer, f"{lname}.{i}", inputs, mappings, weights, awq.duo_scaling, awq.n_grid)
+        rep = awq_mod.awq_layer(layer, checkpoint_name(f"{lname}.{i}", mtype), inputs, mappings, weights,
+                                awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts)
         report[f"{lname}.{i}"] = rep
         nxt = []
         for args, kwargs in inputs:
@@ -130,9 +133,10 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             output_dir: Optional[str] = None, **kwargs) -> nn.Module:
     """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
     scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
-    dataset is already tokenized).  MoE routing during calibration follows the model's own
-    router (``moe_calibrate_all_experts`` applies to AWQ over expert layers, which this round
-    does not smooth -- see DESIGN.md)."""
+    dataset is already tokenized).  ``moe_calibrate_all_experts``: AWQ statistics and loss
+    inputs of expert linears use every calibration token (True, the reference's setting) or
+    only the tokens the router sends to that expert (False); the MoE block's own output is
+    always the routed one (awq.py)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -150,7 +154,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             # embeddings / rotary / final norm run on the device; layers are onloaded one by one
             _to_device_except(model, decoder_layers(model), device)
         for m in awqs:
-            _sequential_awq(model, m, schemes, batches, device, report)
+            _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts)
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
     model.awq_report = report

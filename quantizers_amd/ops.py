@@ -363,8 +363,14 @@ def awq_grid_scales(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio:
 def scale_columns_(w: torch.Tensor, s: torch.Tensor, divide: bool = False) -> torch.Tensor:
     """In place W[:, c] *= s[c] (or /=), bf16-rounded (AWQ _apply_smoothing, balance layers)."""
     _check_dev(w, "weight")
-    w2 = w.reshape(-1, w.shape[-1]) if w.dim() != 1 else w.reshape(1, -1)
     s = s.to(device=w.device, dtype=torch.float32).contiguous()
+    if w.dim() == 3 and not (w.stride(0) == w.shape[1] * w.stride(1)):
+        for wi in w:  # strided batch of slices (fused experts): one launch per slice, in place
+            scale_columns_(wi, s, divide)
+        return w
+    w2 = w.view(-1, w.shape[-1]) if w.dim() == 3 else (w if w.dim() == 2 else w.reshape(1, -1))
+    if w2.stride(-1) != 1:
+        raise ValueError("scale_columns_: rows must be contiguous")
     rc = _lib.load().qz_scale_columns(_ptr(w2), w2.shape[0], w2.shape[1], w2.stride(0), _ptr(s), int(divide),
                                       _stream())
     _lib.check(rc, "qz_scale_columns")

@@ -198,3 +198,113 @@ def test_moe_fused_experts(cuda, tmp_path, recipe, key):
     assert f"model.layers.0.mlp.experts.3.gate_proj.{key}" in sd
     assert not any(k.endswith("experts.gate_up_proj") for k in sd)
     save_compressed(m, str(tmp_path / "moe"))
+
+
+def _minimax(layers=2, experts=8):
+    import warnings
+    from transformers import AutoModelForCausalLM, MiniMaxM2Config
+    cfg = MiniMaxM2Config(hidden_size=128, intermediate_size=64, num_hidden_layers=layers, num_attention_heads=4,
+                          num_key_value_heads=2, head_dim=32, vocab_size=256, num_local_experts=experts,
+                          num_experts_per_tok=2, bos_token_id=1, eos_token_id=2)
+    torch.manual_seed(0)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        m = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("layernorm.weight"):
+                p.copy_((torch.rand_like(p.float()) * 1.5 + 0.25).to(p.dtype))
+    return m
+
+
+def test_minimax_awq_mixedprec_end_to_end(cuda, tmp_path):
+    """recipe_Minimax-M2.1-AWQ-MixedPrec semantics on a tiny random MiniMax-M2: FP8 g32 attention,
+    int4 g32 experts, AWQ over attention, all experts' w1/w3 and each expert's w3 -> w2."""
+    m = _minimax().to(cuda)
+    calib = _calib(vocab=256)
+    ids = torch.stack([c["input_ids"] for c in calib]).to(cuda)
+    with torch.no_grad():
+        ref_logits = m(ids).logits.float()
+    oneshot(m, os.path.join(ROOT, "configs/recipes/minimax_awq_mixedprec.yaml"), dataset=calib, max_seq_length=64)
+    for layer, maps in m.awq_report.items():
+        assert len(maps) == 10, sorted(maps)  # input_ln, post_attn_ln, 8 x w3 (v->o dropped, D9)
+        moe = maps[f"{layer}.post_attention_layernorm"]
+        assert moe["parent"] == f"{layer}.block_sparse_moe" and len(moe["balance"]) == 16
+        for r in maps.values():
+            assert 0.0 <= r["best_ratio"] < 1.0 and len(r["history"]) == 20
+            assert r["best_loss"] <= r["history"][0]
+    with torch.no_grad():
+        new_logits = m(ids).logits.float()
+    rel = (new_logits - ref_logits).norm() / ref_logits.norm()
+    assert rel < 0.05, rel
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 2 * (4 + 24)
+    assert sd["model.layers.1.block_sparse_moe.experts.7.w2.weight_packed"].dtype == torch.int32
+    assert sd["model.layers.0.self_attn.q_proj.weight"].dtype == torch.float8_e4m3fn
+    assert "model.layers.0.block_sparse_moe.gate.weight" in sd
+    assert "model.layers.0.block_sparse_moe.e_score_correction_bias" in sd
+    assert not any(".mlp." in k for k in sd)
+    out = save_compressed(m, str(tmp_path / "mm"))
+    cfg = json.load(open(os.path.join(out, "config.json")))["quantization_config"]
+    assert cfg["format"] == "mixed-precision" and cfg["ignore"] == ["lm_head"]
+
+
+@pytest.mark.parametrize("calibrate_all", [True, False])
+def test_expert_w3_w2_awq_matches_oracle(cuda, calibrate_all):
+    """One expert's w3 -> w2 mapping: statistics over the expert's w2 inputs (all tokens, or the
+    routed ones), w_mean, grid losses and the applied smoothing vs a CPU restatement."""
+    import torch.nn.functional as F
+    from quantizers_amd.awq import awq_layer
+    from quantizers_amd.recipe import AWQMapping
+    from quantizers_amd.quantization import QuantizationArgs
+    m = _minimax(layers=1, experts=4).to(cuda)
+    layer = m.model.layers[0]
+    experts = layer.mlp.experts
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    pre = "model.layers.0.block_sparse_moe.experts"
+    quantized = {f"{pre}.{e}.{p}": a for e in range(4) for p in ("w1", "w2", "w3")}
+    calib = _calib(n=2, s=48, vocab=256)
+    from quantizers_amd.oneshot import _capture_layer0_inputs, _batches
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(calib, None, None, cuda))
+    seen = []
+    h = experts.register_forward_pre_hook(lambda mod, args: seen.append((args[0].clone(), args[1].clone())))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    gu0, down0 = experts.gate_up_proj.data.clone(), experts.down_proj.data.clone()
+    rep = awq_layer(layer, "model.layers.0", inputs, [AWQMapping("re:.*w3$", ["re:.*w2$"])], quantized,
+                    mtype="minimax_m2", calibrate_all_experts=calibrate_all)
+    assert len(rep) == 4
+    oa = ct.QArgs(group_size=32)
+    for e in range(4):
+        with torch.no_grad():
+            hs = []
+            for x, topk in seen:
+                if not calibrate_all:
+                    x = x[(topk == e).any(-1)]
+                g, u = F.linear(x, gu0[e]).chunk(2, dim=-1)
+                hs.append(experts.act_fn(g) * u)
+        s_ref, n_ref = None, 0
+        for t in hs:
+            (s_ref, n_ref) = ct.awq_accumulate_mean(t.cpu(), None if s_ref is None else (s_ref, n_ref))
+        x_mean = s_ref / n_ref
+        w2 = down0[e].cpu()
+        w_mean = ct.awq_layer_means([w2], oa)
+        ref_out = [F.linear(t, down0[e]) for t in hs]
+        cpu_hist = []
+        for i in range(20):
+            s = ct.awq_grid_scales(x_mean, w_mean, i / 20, True)
+            wq = ct.awq_fake_quant_scaled(w2, s, oa).to(cuda)
+            got = [F.linear(t, wq) for t in hs]
+            cpu_hist.append(sum((p - q).float().pow(2).sum().item() for p, q in zip(ref_out, got)) /
+                            sum(p.numel() for p in ref_out))
+        r = rep[f"{pre}.{e}.w3"]
+        torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(cpu_hist), rtol=1e-3, atol=1e-12)
+        best = r["best_ratio"]
+        assert cpu_hist[int(round(best * 20))] <= min(cpu_hist) * 1.001
+        s = ct.awq_grid_scales(x_mean, w_mean, best, True)
+        _eq(experts.down_proj.data[e], (w2.float() * s.view(1, -1)).to(torch.bfloat16), f"w2 smoothed {e}")
+        up0 = gu0[e, 64:].cpu()
+        _eq(experts.gate_up_proj.data[e, 64:], (up0.float() / s.view(-1, 1)).to(torch.bfloat16), f"w3 smoothed {e}")
+        _eq(experts.gate_up_proj.data[e, :64], gu0[e, :64], "w1 untouched")
