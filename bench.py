@@ -139,6 +139,57 @@ def other_configs(ops, QuantizationArgs, dev, gen):
     return res
 
 
+def minimax_pass(ops, QuantizationArgs, dev, gen, world, rank):
+    """BASELINE.json configs[4]: MiniMax-M2.1 mixed precision (recipe_Minimax-M2.1-AWQ-MixedPrec):
+    62 layers x {256 experts x (w1, w3 [1536, 3072], w2 [3072, 1536]) int4 sym g32, attention
+    q [6144, 3072], k/v [1024, 3072], o [3072, 6144] FP8 g32}, layers sharded round-robin over the
+    ranks (strong scaling: the model is fixed).  Two resident synthetic layers are rotated (the
+    whole bf16 model, 460 GB, exceeds one GPU).  Timed between barriers, max over ranks."""
+    i4 = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    f8 = QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32)
+    n_layers, n_exp, hid, inter = 62, 256, 3072, 1536
+    attn = [(6144, hid), (1024, hid), (1024, hid), (hid, 6144)]
+    mine = [l for l in range(n_layers) if l % world == rank]
+    res_layers = []
+    for _ in range(2):
+        gu = (torch.randn(n_exp, 2 * inter, hid, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+        dn = (torch.randn(n_exp, hid, inter, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+        at = [(torch.randn(r, c, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for r, c in attn]
+        res_layers.append((gu, dn, at))
+
+    def run():
+        for j, _ in enumerate(mine):
+            gu, dn, at = res_layers[j % 2]
+            ops.quantize_weight(gu[:, :inter], i4)
+            ops.quantize_weight(gu[:, inter:], i4)
+            ops.quantize_weight(dn, i4)
+            for w in at:
+                ops.quantize_weight(w, f8)
+
+    run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    reps = 2
+    for _ in range(reps):
+        run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / reps], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = t.item()
+    p_exp = n_layers * n_exp * 3 * inter * hid
+    p_att = n_layers * sum(r * c for r, c in attn)
+    del res_layers
+    torch.cuda.empty_cache()
+    return {"params": p_exp + p_att, "ms": t * 1e3, "params_per_s": (p_exp + p_att) / t, "ranks": world,
+            "alg_GBps": (p_exp * (2 + 0.5 + 2 / 32) + p_att * (2 + 1 + 2 / 32)) / t / 1e9,
+            "sharding": "layers round-robin over ranks (strong scaling)"}
+
+
 def read_pmc_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -266,6 +317,7 @@ def main():
     other = None
     if not args.no_model_pass:
         other = other_configs(ops, QuantizationArgs, dev, gen)
+        other["minimax_m2_1_mixedprec_sharded"] = minimax_pass(ops, QuantizationArgs, dev, gen, world, rank)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -38,7 +38,13 @@ def _args_dict(a: Optional[QuantizationArgs]):
 
 
 def quantization_config(model: nn.Module) -> dict:
-    scheme_map: Dict[str, QuantizationScheme] = model.quantization_scheme_map
+    return quantization_config_for(model.quantization_scheme_map,
+                                   [r.name for r in iter_linears(model)])
+
+
+def quantization_config_for(scheme_map: Dict[str, QuantizationScheme], linear_names: List[str]) -> dict:
+    """``config.json.quantization_config`` for the given per-module schemes (unquantized
+    linears are listed under ``ignore``)."""
     groups = {}
     seen = {}
     for name, sch in scheme_map.items():
@@ -51,7 +57,7 @@ def quantization_config(model: nn.Module) -> dict:
                          "input_activations": _args_dict(sch.input_activations),
                          "output_activations": _args_dict(sch.output_activations), "format": fmt}
     fmts = {g["format"] for g in groups.values()}
-    ignore = sorted(r.name for r in iter_linears(model) if r.name not in scheme_map)
+    ignore = sorted(n for n in linear_names if n not in scheme_map)
     return {"config_groups": groups, "format": fmts.pop() if len(fmts) == 1 else "mixed-precision",
             "global_compression_ratio": None, "ignore": ignore, "kv_cache_scheme": None,
             "quant_method": "compressed-tensors", "quantization_status": "compressed",
