@@ -74,6 +74,7 @@ class ResolvedMapping:
     parent: Optional[nn.Module]      # real module re-run for the loss; None = virtual
     parent_kind: str = "module"      # "module" | "linear" (one virtual linear) | "expert" (one expert MLP)
     parent_expert: int = -1
+    origin: int = -1                 # index of the AWQMapping it came from
 
 
 def _common_parent(names: List[str]) -> str:
@@ -98,7 +99,7 @@ def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
     lins = {r.name: r for r in iter_linears(layer, prefix, mtype)}
     virtual = {n: r for n, r in lins.items() if r.index is not None}
     out: List[ResolvedMapping] = []
-    for mp in mappings:
+    for mi, mp in enumerate(mappings):
         srx = _rx(mp.smooth_layer)
         snames = [n for n in mods if re.match(srx, n)] + [n for n in virtual if re.match(srx, n)]
         for sname in snames:
@@ -126,9 +127,10 @@ def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
             if len(balance) == 1:
                 pname = balance[0]
                 if refs[0].index is None:
-                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, refs[0].module))
+                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, refs[0].module, origin=mi))
                 else:
-                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, None, "linear", refs[0].index[0]))
+                    out.append(ResolvedMapping(sname, smooth, balance, refs, pname, None, "linear", refs[0].index[0],
+                                               origin=mi))
                 continue
             pname = _common_parent(balance)
             kind, expert = "module", -1
@@ -142,7 +144,7 @@ def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
                     break
                 pname = pname.rpartition(".")[0]
             out.append(ResolvedMapping(sname, smooth, balance, refs, pname, mods.get(pname) if kind == "module" else None,
-                                       kind, expert))
+                                       kind, expert, origin=mi))
     return out
 
 
@@ -273,6 +275,50 @@ def _view(g: List[LinearRef]) -> torch.Tensor:
     return g[0].weight if len(g) == 1 else stacked_view(g)
 
 
+def _independent_batches(resolved: List[ResolvedMapping]) -> List[List[ResolvedMapping]]:
+    """Split the mapping sequence into runs whose grid searches do not depend on each other's
+    smoothing: consecutive mappings from one AWQMapping entry whose loss parent is their single
+    balance layer and whose smooth/balance layers are all distinct (per-expert w3 -> w2,
+    up -> down of every expert).  Everything else stays a run of one, in order."""
+    out: List[List[ResolvedMapping]] = []
+    for r in resolved:
+        single = len(r.balance) == 1 and r.parent_kind in ("linear", "module") and \
+            r.parent_name == r.balance_names[0]
+        if out and single and len(out[-1]) >= 1:
+            prev = out[-1]
+            p = prev[0]
+            p_single = len(p.balance) == 1 and p.parent_name == p.balance_names[0]
+            touched = {x.smooth_name for x in prev} | {x.balance_names[0] for x in prev}
+            if p_single and p.origin == r.origin and r.smooth_name not in touched and \
+                    r.balance_names[0] not in touched:
+                prev.append(r)
+                continue
+        out.append([r])
+    return out
+
+
+def _sharded_search(batch: List[ResolvedMapping], search) -> List[Any]:
+    """Run ``search`` over a batch of independent mappings; under torch.distributed each rank
+    takes every world-th mapping and the results (ratio, loss, history, scale vector) are
+    all-gathered, so every rank applies identical smoothing (bit-identical to one process)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [search(r) for r in batch]
+    world, rank = dist.get_world_size(), dist.get_rank()
+    mine = {}
+    for k in range(rank, len(batch), world):
+        f = search(batch[k])
+        mine[k] = None if f is None else (f[0], f[1], f[2], f[3].cpu())
+    gathered: List[Any] = [None] * world
+    dist.all_gather_object(gathered, mine)
+    dev = batch[0].balance[0].weight.device
+    found: List[Any] = [None] * len(batch)
+    for part in gathered:
+        for k, f in part.items():
+            found[k] = None if f is None else (f[0], f[1], f[2], f[3].to(dev))
+    return found
+
+
 @torch.no_grad()
 def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dict]], mappings: List[AWQMapping],
               quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20,
@@ -310,8 +356,9 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     for ei in experts.values():
         ei.snapshot()
     n_batches = len(layer_inputs)
-    report = {}
-    for r in resolved:
+
+    def search(r: ResolvedMapping):
+        """Grid search of one mapping; returns (best_ratio, best_loss, history, best_scales) or None."""
         b0 = r.balance[0]
         if b0.index is None:
             x_mean = stats[r.smooth_name].mean()
@@ -322,8 +369,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                 am.add(_virtual_input(ei, b0, i))
             if am.count == 0:  # expert never routed to (moe_calibrate_all_experts=False)
                 log.info("AWQ: skipping mapping %s (no calibration tokens)", r.smooth_name)
-                report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "skipped": "no tokens"}
-                continue
+                return None
             x_mean = am.mean()
         groups = _launch_groups(r, quantized)
         # 2. w_mean over the balance layers (each with its own group size)
@@ -377,9 +423,15 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             raise RuntimeError(f"AWQ: no finite loss for {r.smooth_name} (history {history})")
         best, best_i = min(finite)  # first best ratio (strict <): min over (loss, index)
         best_ratio = best_i / n_grid
-        best_scales = ops.awq_grid_scales(x_mean, w_mean, best_ratio, duo_scaling)
-        # 4. apply smoothing
-        for g in groups:
+        return best_ratio, best, history, ops.awq_grid_scales(x_mean, w_mean, best_ratio, duo_scaling)
+
+    def apply(r: ResolvedMapping, found):
+        """4. _apply_smoothing: balance columns *= s, smooth rows (and bias) /= s."""
+        if found is None:
+            report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "skipped": "no tokens"}
+            return
+        best_ratio, best, history, best_scales = found
+        for g in _launch_groups(r, quantized):
             ops.scale_columns_(_view(g), best_scales, divide=False)
         sw = r.smooth.weight if isinstance(r.smooth, LinearRef) else r.smooth.weight.data
         if sw.dim() == 1:
@@ -391,5 +443,15 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             ops.scale_rows_(b.data[-best_scales.numel():], best_scales, divide=True)
         report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "best_ratio": best_ratio,
                                  "best_loss": best, "history": history}
-        del ref_out, orig, tmp
+
+    report: Dict[str, Any] = {}
+    for batch in _independent_batches(resolved):
+        if len(batch) == 1:
+            apply(batch[0], search(batch[0]))
+            continue
+        # mutually independent single-layer-parent mappings (e.g. every expert's w3 -> w2):
+        # search all (sharded over ranks under torch.distributed), then smooth in order
+        found = _sharded_search(batch, search)
+        for r, f in zip(batch, found):
+            apply(r, f)
     return report

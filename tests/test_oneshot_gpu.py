@@ -308,3 +308,36 @@ def test_expert_w3_w2_awq_matches_oracle(cuda, calibrate_all):
         up0 = gu0[e, 64:].cpu()
         _eq(experts.gate_up_proj.data[e, 64:], (up0.float() / s.view(-1, 1)).to(torch.bfloat16), f"w3 smoothed {e}")
         _eq(experts.gate_up_proj.data[e, :64], gu0[e, :64], "w1 untouched")
+
+
+def _awq_rank(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _minimax(experts=8).to("cuda:0")
+        oneshot(m, os.path.join(ROOT, "configs/recipes/minimax_experts_awq.yaml"), dataset=_calib(vocab=256),
+                max_seq_length=64)
+        if rank == 1:
+            torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_expert_awq_sharded_two_ranks(cuda, tmp_path):
+    """Per-expert w3 -> w2 searches sharded over 2 ranks (gloo control plane, one card): the
+    smoothed model is bit-identical to the one-process run."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rank1.pt")
+    mp.spawn(_awq_rank, args=(2, port, out), nprocs=2, join=True)
+    m = _minimax(experts=8).to(cuda)
+    oneshot(m, os.path.join(ROOT, "configs/recipes/minimax_experts_awq.yaml"), dataset=_calib(vocab=256),
+            max_seq_length=64)
+    two = torch.load(out, weights_only=True)
+    for k, v in m.state_dict().items():
+        _eq(v, two[k], k)
+    assert len(m.awq_report["model.layers.0"]) == 9
