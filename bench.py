@@ -33,7 +33,7 @@ PARAMS = ROWS * COLS
 ALG_BYTES = PARAMS * 2 + PARAMS * BITS // 8 + (PARAMS // GROUP) * 2  # 113,426,432
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128"
-KERNEL_NAME = "k_group_fast<4, 0, false>"
+KERNEL_NAME = "k_group_fast<4, 0, false, true, false>"
 
 # Qwen3-4B linear shapes (hidden 2560, inter 9728, 32 q / 8 kv heads x 128), 36 layers
 QWEN3_4B = [("q_proj", 4096, 2560), ("k_proj", 1024, 2560), ("v_proj", 1024, 2560), ("o_proj", 2560, 4096),

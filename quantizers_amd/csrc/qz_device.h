@@ -169,8 +169,10 @@ __device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, floa
     if (sf == 0.f) { s8 = 0x20u; sf = 0.125f; }  // eps of float8_e4m3fn
     g.sbits = s8;
     g.s = sf / gs;  // _quantize: scale / global_scale (f32)
-    g.rs = 0.f;
-    g.fast = false;  // f32 quotient: IEEE division per element
+    // f32 quotient x / s: the fast kernel forms x * rs and falls back to the IEEE division
+    // only when x * rs is within a few ulps of an E2M1 rounding boundary (encode_store)
+    g.rs = __builtin_amdgcn_rcpf(g.s);  // approximate (1 ulp): only steers the fast path
+    g.fast = (g.s >= 0x1.0p-100f) && (g.s <= 0x1.0p+100f);
     return g;
   }
   if (s == 0.f) s = 0.0078125f;  // D1: finfo(bf16).eps

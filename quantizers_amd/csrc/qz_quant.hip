@@ -25,7 +25,11 @@ constexpr int BLOCK = 256;
 #ifndef QZ_UNROLL
 #define QZ_UNROLL 2
 #endif
-constexpr int UNROLL = QZ_UNROLL;  // 16-B loads per lane per tile (x2 in flight when pipelined)
+constexpr int UNROLL = QZ_UNROLL;  // 16-B units per lane per tile
+#ifndef QZ_FAST_BLOCK
+#define QZ_FAST_BLOCK 128
+#endif
+constexpr int FBLOCK = QZ_FAST_BLOCK;  // threads per workgroup of the group path (one tile per wave)
 #ifndef QZ_NUM_CUS
 #define QZ_NUM_CUS 256  // MI355X
 #endif
@@ -108,6 +112,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef QZ_HW_FP4
 #define QZ_HW_FP4 1
 #endif
+#ifndef QZ_NT_BYTES
+#define QZ_NT_BYTES (256ll << 20)  // weight bytes per launch above which loads are non-temporal
+#endif
 #ifndef QZ_LDS_AUX
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
@@ -126,6 +133,31 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
 template <int KIND, bool FQ, bool SYM>
 __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, const GP& g, const f32x2* x,
                                              const f32x2* cs, const int64_t unit) {
+
+  // ---- NVFP4, quantize only: the f32 quotient x / s is decided from q = x * rcp(s), which is
+  // within 3 ulps of it.  The E2M1 rounding boundaries (0.25 0.75 1.25 1.75 2.5 3.5 5) have
+  // only their top 2 mantissa bits set, so q can round differently from x / s only if its low
+  // 21 mantissa bits are within 4 of zero (mod 2^21); such pairs (and +-0, which needs the
+  // signed-zero rule) take the IEEE division.  Exact grid values may be flagged too (harmless).
+  if (KIND == K_NV && !FQ && QZ_HW_FP4) {
+    uint32_t word = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float qa = x[k].x * g.rs, qb = x[k].y * g.rs;
+      const bool near = (((__float_as_uint(qa) + 4u) & 0x1fffffu) < 8u) | (((__float_as_uint(qb) + 4u) & 0x1fffffu) < 8u);
+      uint32_t pk;
+      if (__builtin_expect(near || !g.fast, 0)) {
+        pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, __builtin_amdgcn_fmed3f(x[k].x / g.s, -6.f, 6.f) + 0.0f,
+                                                      __builtin_amdgcn_fmed3f(x[k].y / g.s, -6.f, 6.f) + 0.0f, 1.0f, 0);
+      } else {
+        pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, __builtin_amdgcn_fmed3f(qa, -6.f, 6.f),
+                                                      __builtin_amdgcn_fmed3f(qb, -6.f, 6.f), 1.0f, 0);
+      }
+      word |= (pk & 0xffu) << (8 * k);
+    }
+    reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
+    return;
+  }
 
   // ---- quotient x / scale (bf16; f32 for NVFP4); x * rcp(s) is exact-equivalent (rcp lemma)
   f32x2 t[4];
@@ -342,12 +374,12 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
 // persistent grid-stride loop with register double-buffering is slower than one-shot waves.
 // Out-of-range lanes re-load the slice's last unit (results never stored), keeping the
 // loads branch-free.  grid = (tiles per slice, batch): slices may be strided (fused experts).
-template <int LOGL, int KIND, bool FQ, bool SYM>
-__global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
-  __shared__ uint4 lds_buf[BLOCK / WAVE][UNROLL][WAVE];
+template <int LOGL, int KIND, bool FQ, bool SYM, bool NT = false>
+__global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
+  __shared__ uint4 lds_buf[FBLOCK / WAVE][UNROLL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * (BLOCK / WAVE) + w;
+  const int64_t tile = (int64_t)blockIdx.x * (FBLOCK / WAVE) + w;
   const int64_t tiles = (A.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
   if (tile >= tiles) return;
   const int64_t b = blockIdx.y;
@@ -357,7 +389,8 @@ __global__ __launch_bounds__(BLOCK) void k_group_fast(FastArgs A) {
     int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
     unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
     __builtin_amdgcn_global_load_lds((const void*)(src + unit),
-                                     (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0, QZ_LDS_AUX);
+                                     (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
+                                     NT ? 2 : QZ_LDS_AUX);
   }
   QP p = A.p;
   p.kind = KIND;
@@ -531,6 +564,42 @@ __global__ __launch_bounds__(BLOCK) void k_minmax_generic(GenArgs A, uint32_t* k
 
 // NVFP4 global scale per batch item: (448*6)/absmax in bf16 as reciprocal-then-multiply
 // (python-scalar / tensor == tensor.reciprocal() * scalar), then widened to f32.
+// Per-slice |w| maximum (NVFP4's per-tensor observer) for dense, 16-B aligned slices: 16-B
+// loads, 4 in flight per lane, v_pk_max_u16 on |bf16| bit patterns, wave DPP max, one atomic per
+// workgroup.  tmin/tmax receive the keys of -absmax / +absmax (all k_gscale_keys needs).
+__global__ __launch_bounds__(256) void k_absmax_slices(const uint16_t* w, int64_t units_per_batch, int64_t ld_batch,
+                                                       uint32_t* tmin, uint32_t* tmax) {
+  const int64_t b = blockIdx.y;
+  const uint4* src = reinterpret_cast<const uint4*>(w + b * ld_batch);
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  uint32_t m = 0;
+  int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  for (; u + 3 * stride < units_per_batch; u += 4 * stride) {
+    uint4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = src[u + j * stride];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      m = pk_max_u16(m, pk_max_u16(pk_max_u16(v[j].x & 0x7fff7fffu, v[j].y & 0x7fff7fffu),
+                                   pk_max_u16(v[j].z & 0x7fff7fffu, v[j].w & 0x7fff7fffu)));
+  }
+  for (; u < units_per_batch; u += stride) {
+    const uint4 v = src[u];
+    m = pk_max_u16(m, pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu),
+                                 pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu)));
+  }
+  m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
+  __shared__ uint32_t red[256 / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = max(max(red[0], red[1]), max(red[2], red[3]));
+    const float am = __uint_as_float(m << 16);
+    atomicMax(tmax + b, f2key(am));
+    atomicMin(tmin + b, f2key(-am));
+  }
+}
+
 __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_t batch, float* gs) {
   int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= batch) return;
@@ -665,29 +734,32 @@ __global__ void k_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int bi
 // ---------------------------------------------------------------------- host side
 using FastFn = void (*)(FastArgs);
 
+// fq: AWQ fake-quant; nt: non-temporal weight stream (launches much larger than the 256 MiB
+// Infinity Cache: the read-once weight should not evict the outputs; +6 % at 360 MB, -2 % at 90 MB)
 template <int LOGL, int KIND, bool SYM>
-FastFn pick_fq(bool fq) {
-  return fq ? (FastFn)k_group_fast<LOGL, KIND, true, SYM> : (FastFn)k_group_fast<LOGL, KIND, false, SYM>;
+FastFn pick_fq(bool fq, bool nt) {
+  if (fq) return k_group_fast<LOGL, KIND, true, SYM>;
+  return nt ? (FastFn)k_group_fast<LOGL, KIND, false, SYM, true> : (FastFn)k_group_fast<LOGL, KIND, false, SYM>;
 }
 template <int LOGL>
-FastFn pick_kind(int kind, bool sym, bool fq) {
+FastFn pick_kind(int kind, bool sym, bool fq, bool nt) {
   switch (kind) {
-    case K_INT: return sym ? pick_fq<LOGL, K_INT, true>(fq) : pick_fq<LOGL, K_INT, false>(fq);
-    case K_FP8: return pick_fq<LOGL, K_FP8, true>(fq);
-    case K_MX: return pick_fq<LOGL, K_MX, true>(fq);
-    case K_NV: return pick_fq<LOGL, K_NV, true>(fq);
-    default: return pick_fq<LOGL, K_FP4, true>(fq);
+    case K_INT: return sym ? pick_fq<LOGL, K_INT, true>(fq, nt) : pick_fq<LOGL, K_INT, false>(fq, nt);
+    case K_FP8: return pick_fq<LOGL, K_FP8, true>(fq, nt);
+    case K_MX: return pick_fq<LOGL, K_MX, true>(fq, nt);
+    case K_NV: return pick_fq<LOGL, K_NV, true>(fq, nt);
+    default: return pick_fq<LOGL, K_FP4, true>(fq, nt);
   }
 }
-FastFn pick_fast(int logl, int kind, bool sym, bool fq) {
+FastFn pick_fast(int logl, int kind, bool sym, bool fq, bool nt) {
   switch (logl) {
-    case 0: return pick_kind<0>(kind, sym, fq);
-    case 1: return pick_kind<1>(kind, sym, fq);
-    case 2: return pick_kind<2>(kind, sym, fq);
-    case 3: return pick_kind<3>(kind, sym, fq);
-    case 4: return pick_kind<4>(kind, sym, fq);
-    case 5: return pick_kind<5>(kind, sym, fq);
-    default: return pick_kind<6>(kind, sym, fq);
+    case 0: return pick_kind<0>(kind, sym, fq, nt);
+    case 1: return pick_kind<1>(kind, sym, fq, nt);
+    case 2: return pick_kind<2>(kind, sym, fq, nt);
+    case 3: return pick_kind<3>(kind, sym, fq, nt);
+    case 4: return pick_kind<4>(kind, sym, fq, nt);
+    case 5: return pick_kind<5>(kind, sym, fq, nt);
+    default: return pick_kind<6>(kind, sym, fq, nt);
   }
 }
 
@@ -907,7 +979,17 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     GenArgs T = G;
     T.strategy = QZ_TENSOR;
     T.ng_item = 1;
-    if ((rc = run_minmax(T, batch, W.tmin, W.tmax, st))) return rc;
+    if (!col_scales && rows_dense && aligned(w, 16) && cols % 8 == 0 && (batch == 1 || ld_batch % 8 == 0) &&
+        batch <= 65535) {  // (AWQ's fake-quant observes W * s: generic path)
+      const int64_t ups = rows * cols / 8;
+      const int64_t chunks = std::max<int64_t>(1, std::min<int64_t>(cdiv(ups, 256 * 4), cdiv(2048, batch)));
+      hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)cdiv(batch, 256)), dim3(256), 0, st, W.tmin, batch, 0xffffffffu);
+      hipLaunchKernelGGL(k_fill_u32, dim3((unsigned)cdiv(batch, 256)), dim3(256), 0, st, W.tmax, batch, 0u);
+      hipLaunchKernelGGL(k_absmax_slices, dim3((unsigned)chunks, (unsigned)batch), dim3(256), 0, st,
+                         (const uint16_t*)w, ups, batch > 1 ? ld_batch : rows * cols, W.tmin, W.tmax);
+    } else if ((rc = run_minmax(T, batch, W.tmin, W.tmax, st))) {
+      return rc;
+    }
     hipLaunchKernelGGL(k_gscale_keys, dim3((unsigned)cdiv(batch, 64)), dim3(64), 0, st, W.tmin, W.tmax, batch, gs_dst);
     if ((rc = launch_err())) return rc;
   }
@@ -935,8 +1017,10 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const int64_t n_tiles = cdiv(F.units_per_batch, UNROLL * WAVE);
-    const int64_t blocks = cdiv(n_tiles, BLOCK / WAVE);
-    hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq), dim3((unsigned)blocks, (unsigned)batch), dim3(BLOCK), 0, st, F);
+    const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
+    const bool nt = batch * rows * cols * 2 > QZ_NT_BYTES;
+    hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
+                       dim3(FBLOCK), 0, st, F);
     return launch_err();
   }
 

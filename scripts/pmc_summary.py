@@ -13,7 +13,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "k_group_fast<4, 0, false, true>"
+KERNEL = "k_group_fast<4, 0, false, true, false>"
 ALG = 113426432
 
 
