@@ -190,6 +190,46 @@ def minimax_pass(ops, QuantizationArgs, dev, gen, world, rank):
             "sharding": "layers round-robin over ranks (strong scaling)"}
 
 
+def _event_us(fn, n, stream):
+    """Mean per-launch duration (HIP events on the launch stream) of fn(i), i = 0..n-1."""
+    for i in range(3):
+        fn(i)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for i in range(n):
+        ev[i][0].record(stream)
+        fn(i)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    return sum(a.elapsed_time(b) for a, b in ev) / n * 1e3
+
+
+def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream):
+    """The AWQ kernels on the headline weight shape, each with its
+    algorithmic bytes and achieved HBM GB/s (rotating the HBM-resident weight copies)."""
+    a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, group_size=GROUP)
+    nc = len(copies)
+    s = torch.rand(COLS, device=dev, generator=gen) + 0.5
+    fq_out = torch.empty_like(copies[0])
+    x = [(torch.randn(16384, COLS, device=dev, generator=gen)).to(torch.bfloat16) for _ in range(4)]
+    sums = torch.zeros(COLS, dtype=torch.float32, device=dev)
+    wsum = torch.zeros(COLS, dtype=torch.float64, device=dev)
+    res = {}
+    for name, fn, nbytes in [
+        ("fake_quant_scaled (a5: Q(W*s)/s, int4 g128)",
+         lambda i: ops.fake_quantize(copies[i % nc], a, col_scales=s, out=fq_out), PARAMS * 4 + COLS * 4),
+        ("absmean_accum (a3: sum|x| over [16384, 4096] activations)",
+         lambda i: ops.awq_absmean_accum(x[i % 4], sums), x[0].numel() * 2),
+        ("weight_mean_accum (a4: |W|/group absmax, g128)",
+         lambda i: ops.awq_weight_mean_accum(copies[i % nc], GROUP, wsum), PARAMS * 2),
+        ("scale_columns (a6: W[:, c] *= s[c])",
+         lambda i: ops.scale_columns_(copies[i % nc], s), PARAMS * 4),
+    ]:
+        us = _event_us(fn, 40, stream)
+        res[name] = {"us": us, "alg_bytes": nbytes, "GBps": nbytes / (us * 1e-6) / 1e9}
+    del x
+    return res
+
+
 def read_pmc_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -292,6 +332,11 @@ def main():
         torch.cuda.synchronize()
         allgather = (time.perf_counter() - ta) / reps * 1e3
 
+    # ---- the AWQ kernels (a3-a6) on the same resident weights
+    awq = None
+    if not args.no_model_pass:
+        awq = awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream)
+
     # ---- whole-model pass: every Qwen3-4B linear (36 layers, batched per shape)
     model_pass = None
     if not args.no_model_pass:
@@ -354,6 +399,7 @@ def main():
             "parity_check": ok,
             "allgather_ms": allgather,
             "qwen3_4b_all_linears": model_pass,
+            "awq_kernels": awq,
             "other_configs": other,
         }
         print(json.dumps(line), flush=True)
