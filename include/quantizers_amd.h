@@ -180,6 +180,16 @@ int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channel
                        qz_stream_t stream);
 
 /*
+ * qz_awq_grid_scales_batched -- the same grid point for `batch` independent mappings at once
+ * (x_mean / w_mean / scales_out are [batch, channels], row-major): every MoE expert's
+ * w3 -> w2 (up_proj -> down_proj) mapping of one layer in one launch.  Results are identical
+ * to `batch` calls of qz_awq_grid_scales.
+ */
+int qz_awq_grid_scales_batched(const float* x_mean, const float* w_mean, int64_t batch,
+                               int64_t channels, float ratio, int32_t duo_scaling,
+                               float* scales_out, qz_stream_t stream);
+
+/*
  * qz_awq_fake_quant -- the grid search's per-balance-layer step W' = Q(W * s) / s with the
  * layer's own scheme, fused into one pass (bf16 products, bf16 fake-quant, f32 column
  * scales).  col_scales may be NULL (plain fake_quantize).  w_out may alias w.
@@ -187,6 +197,16 @@ int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channel
 int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
                       int64_t ld_batch, const qz_args* a, const float* col_scales, void* w_out,
                       void* workspace, size_t workspace_bytes, qz_stream_t stream);
+
+/*
+ * qz_awq_fake_quant_batched -- qz_awq_fake_quant over a batch of slices with one column-scale
+ * vector per slice: col_scales[b * cs_ld_batch + c] (cs_ld_batch >= cols; 0 = shared).  The
+ * batched grid step of per-expert AWQ mappings (each expert's w2 with its own scales).
+ */
+int qz_awq_fake_quant_batched(const void* w, int64_t batch, int64_t rows, int64_t cols,
+                              int64_t ld_row, int64_t ld_batch, const qz_args* a,
+                              const float* col_scales, int64_t cs_ld_batch, void* w_out,
+                              void* workspace, size_t workspace_bytes, qz_stream_t stream);
 
 /*
  * qz_scale_columns / qz_scale_rows -- AWQ _apply_smoothing: in place, bf16-rounded,

@@ -297,26 +297,46 @@ def _independent_batches(resolved: List[ResolvedMapping]) -> List[List[ResolvedM
     return out
 
 
-def _sharded_search(batch: List[ResolvedMapping], search) -> List[Any]:
-    """Run ``search`` over a batch of independent mappings; under torch.distributed each rank
-    takes every world-th mapping and the results (ratio, loss, history, scale vector) are
-    all-gathered, so every rank applies identical smoothing (bit-identical to one process)."""
+def _sharded_search(batch: List[ResolvedMapping], search_chunk, chunk: int = 1) -> List[Any]:
+    """Run ``search_chunk`` (a list of mappings -> a list of results) over consecutive chunks of
+    a batch of independent mappings; under torch.distributed rank r takes chunks r, r + world,
+    ... and the results (ratio, loss, history, scale vector) are all-gathered, so every rank
+    applies identical smoothing.  Chunk boundaries do not depend on the world size, so the
+    result is bit-identical to one process."""
     import torch.distributed as dist
+    chunks = [batch[i:i + chunk] for i in range(0, len(batch), chunk)]
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-        return [search(r) for r in batch]
+        return [f for c in chunks for f in search_chunk(c)]
     world, rank = dist.get_world_size(), dist.get_rank()
     mine = {}
-    for k in range(rank, len(batch), world):
-        f = search(batch[k])
-        mine[k] = None if f is None else (f[0], f[1], f[2], f[3].cpu())
+    for j in range(rank, len(chunks), world):
+        mine[j] = [None if f is None else (f[0], f[1], f[2], f[3].cpu()) for f in search_chunk(chunks[j])]
     gathered: List[Any] = [None] * world
     dist.all_gather_object(gathered, mine)
     dev = batch[0].balance[0].weight.device
-    found: List[Any] = [None] * len(batch)
+    per_chunk: Dict[int, List[Any]] = {}
     for part in gathered:
-        for k, f in part.items():
-            found[k] = None if f is None else (f[0], f[1], f[2], f[3].to(dev))
-    return found
+        per_chunk.update(part)
+    return [None if f is None else (f[0], f[1], f[2], f[3].to(dev)) for j in range(len(chunks)) for f in per_chunk[j]]
+
+
+def _expert_batchable(batch: List[ResolvedMapping], quantized: Dict[str, QuantizationArgs], calibrate_all: bool) -> bool:
+    """Every expert's w3 -> w2 of one fused module, one scheme: searchable as batched launches."""
+    if not calibrate_all or len(batch) < 2:
+        return False
+    r0 = batch[0]
+    b0 = r0.balance[0]
+    if r0.parent_kind != "linear" or b0.param_name not in ("down_proj", "w2"):
+        return False
+    return all(r.parent_kind == "linear" and r.balance[0].module is b0.module and
+               r.balance[0].param_name == b0.param_name and
+               quantized[r.balance_names[0]] is quantized[r0.balance_names[0]] for r in batch)
+
+
+def _expert_chunk(n_tokens: int, inter: int, hidden: int, budget: int = 4 << 30) -> int:
+    """Experts per batched search chunk: their w2 inputs and reference outputs stay resident."""
+    per_expert = n_tokens * (inter + hidden) * 2
+    return int(max(1, min(16, budget // max(per_expert, 1))))
 
 
 @torch.no_grad()
@@ -444,6 +464,55 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         report[r.smooth_name] = {"balance": r.balance_names, "parent": r.parent_name, "best_ratio": best_ratio,
                                  "best_loss": best, "history": history}
 
+    def search_experts(chunk: List[ResolvedMapping]):
+        """Grid search of several experts' w3 -> w2 mappings at once: w2 inputs recomputed per
+        expert (as in ``search``), then per grid point ONE batched scale launch, ONE batched
+        fake-quant launch (one scale vector per expert) and one GEMM per expert over all its
+        calibration tokens; per-expert losses stay on the device."""
+        refs = [r.balance[0] for r in chunk]
+        mod, pname = refs[0].module, refs[0].param_name
+        ei = experts[id(mod)]
+        a = quantized[chunk[0].balance_names[0]]
+        es = [ref.index[0] for ref in refs]
+        w2 = getattr(mod, pname).data  # [E, H, I]
+        hid = [[_virtual_input(ei, ref, i) for i in range(n_batches)] for ref in refs]  # [e][i] -> [T_i, I]
+        cols = w2.shape[2]
+        xm = torch.empty(len(refs), cols, dtype=torch.float32, device=w2.device)
+        wm = torch.empty_like(xm)
+        for k, ref in enumerate(refs):
+            am = _AbsMean()
+            for t in hid[k]:
+                am.add(t)
+            xm[k] = am.mean()
+            wsum = torch.zeros(cols, dtype=torch.float64, device=w2.device)
+            rows = ops.awq_weight_mean_accum(ref.weight, _group_size_for_mean(a, cols), wsum)
+            wm[k] = (wsum / rows).float()
+        # all calibration tokens of an expert in one [T, I] operand: one GEMM per expert and
+        # grid point (2-D GEMMs: the path every other mapping uses)
+        hs = [torch.cat(h) if len(h) > 1 else h[0] for h in hid]
+        del hid
+        w0 = torch.stack([w2[e] for e in es])  # [k, H, I] (pre-search weights)
+        ref_out = [nn.functional.linear(h, w0[k]) for k, h in enumerate(hs)]
+        n_el = ref_out[0].numel()
+        wq = torch.empty_like(w0)
+        scales = torch.empty(n_grid, len(refs), cols, dtype=torch.float32, device=w2.device)
+        losses = torch.zeros(n_grid, len(refs), dtype=torch.float64, device=w2.device)
+        for g in range(n_grid):
+            ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
+            ops.fake_quantize_batched(w0, a, scales[g], out=wq)
+            for k, (h, ro) in enumerate(zip(hs, ref_out)):
+                losses[g, k] = (ro - nn.functional.linear(h, wq[k])).float().pow(2).sum().double()
+        hist = (losses / max(n_el, 1)).cpu()
+        out = []
+        for k in range(len(refs)):
+            history = hist[:, k].tolist()
+            finite = [(l, i) for i, l in enumerate(history) if l == l]
+            if not finite:
+                raise RuntimeError(f"AWQ: no finite loss for {chunk[k].smooth_name} (history {history})")
+            best, bi = min(finite)
+            out.append((bi / n_grid, best, history, scales[bi, k].clone()))
+        return out
+
     report: Dict[str, Any] = {}
     for batch in _independent_batches(resolved):
         if len(batch) == 1:
@@ -451,7 +520,14 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             continue
         # mutually independent single-layer-parent mappings (e.g. every expert's w3 -> w2):
         # search all (sharded over ranks under torch.distributed), then smooth in order
-        found = _sharded_search(batch, search)
+        if _expert_batchable(batch, quantized, calibrate_all_experts):
+            b0 = batch[0].balance[0]
+            ei = experts[id(b0.module)]
+            n_tok = sum(x.shape[0] for x in ei.x)
+            w2 = getattr(b0.module, b0.param_name)
+            found = _sharded_search(batch, search_experts, _expert_chunk(n_tok, w2.shape[2], w2.shape[1]))
+        else:
+            found = _sharded_search(batch, lambda c: [search(c[0])])
         for r, f in zip(batch, found):
             apply(r, f)
     return report

@@ -133,6 +133,10 @@ __device__ __forceinline__ float nmin(float a, float b) { return (a != a || b !=
 
 __global__ __launch_bounds__(1024) void k_grid_scales(const float* xm, const float* wm, int64_t C, float ratio,
                                                       int duo, float* out) {
+  // one workgroup per scale vector (blockIdx.x = batch item: one MoE expert's mapping)
+  xm += (int64_t)blockIdx.x * C;
+  if (wm) wm += (int64_t)blockIdx.x * C;
+  out += (int64_t)blockIdx.x * C;
   __shared__ float smx[16], smn[16];
   float lmx = -INFINITY, lmn = INFINITY;
   for (int64_t c = threadIdx.x; c < C; c += 1024) {
@@ -250,6 +254,15 @@ int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channel
   if (channels <= 0 || channels > 65536) return QZ_ERR_SHAPE;
   hipLaunchKernelGGL(k_grid_scales, dim3(1), dim3(1024), 0, (hipStream_t)stream, x_mean, w_mean, channels, ratio,
                      (int)duo_scaling, scales_out);
+  return launch_err();
+}
+
+int qz_awq_grid_scales_batched(const float* x_mean, const float* w_mean, int64_t batch, int64_t channels,
+                               float ratio, int32_t duo_scaling, float* scales_out, qz_stream_t stream) {
+  if (!x_mean || !scales_out || (duo_scaling && !w_mean)) return QZ_ERR_NULL;
+  if (channels <= 0 || channels > 65536 || batch <= 0 || batch > 65535) return QZ_ERR_SHAPE;
+  hipLaunchKernelGGL(k_grid_scales, dim3((unsigned)batch), dim3(1024), 0, (hipStream_t)stream, x_mean, w_mean,
+                     channels, ratio, (int)duo_scaling, scales_out);
   return launch_err();
 }
 

@@ -99,7 +99,8 @@ struct FastArgs {
   void* s_out;
   int8_t* zp_out;
   const float* gscale;      // [batch], NVFP4
-  const float* col_scales;  // [cols], AWQ prescale (FQ only)
+  const float* col_scales;  // [cols] (+ b * cs_ld_batch), AWQ prescale (FQ only)
+  int64_t cs_ld_batch;      // 0: one scale vector for every slice; cols: one per slice
 };
 
 // --------------------------------------------------------------- single-pass path
@@ -283,7 +284,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
 // Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
 template <int LOGL, int KIND, bool FQ, bool SYM>
 __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
-                                             const bool valid, const float gs, const int lane) {
+                                             const bool valid, const float gs, const int lane, const int64_t b) {
   constexpr int L = 1 << LOGL;
   // unit: dense output index (batch*units_per_batch + local); valid is uniform within a group
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
@@ -295,9 +296,10 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
   f32x2 cs[4];
   if (FQ && A.col_scales) {
+    const float* cs_b = A.col_scales + b * A.cs_ld_batch;
     const int64_t c0 = (unit % A.units_per_row) * 8;
-    const float4 c_lo = *reinterpret_cast<const float4*>(A.col_scales + c0);
-    const float4 c_hi = *reinterpret_cast<const float4*>(A.col_scales + c0 + 4);
+    const float4 c_lo = *reinterpret_cast<const float4*>(cs_b + c0);
+    const float4 c_hi = *reinterpret_cast<const float4*>(cs_b + c0 + 4);
     cs[0] = f32x2{c_lo.x, c_lo.y}; cs[1] = f32x2{c_lo.z, c_lo.w};
     cs[2] = f32x2{c_hi.x, c_hi.y}; cs[3] = f32x2{c_hi.z, c_hi.w};
 #pragma unroll
@@ -361,7 +363,7 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
       if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
     }
 #else
-    process_unit<LOGL, KIND, FQ, SYM>(A, p, v[u], unit, valid, gs, lane);
+    process_unit<LOGL, KIND, FQ, SYM>(A, p, v[u], unit, valid, gs, lane, b);
 #endif
   }
 }
@@ -491,6 +493,7 @@ struct GenArgs {
   int64_t bh, bw;  // BLOCK
   int64_t ng_item; // groups per batch item
   const float* col_scales;
+  int64_t cs_ld_batch;  // col_scales stride between batch items (0: shared)
 };
 
 __device__ __forceinline__ int64_t group_of(const GenArgs& A, int64_t r, int64_t c) {
@@ -504,7 +507,7 @@ __device__ __forceinline__ int64_t group_of(const GenArgs& A, int64_t r, int64_t
 
 __device__ __forceinline__ float load_w(const GenArgs& A, int64_t b, int64_t r, int64_t c) {
   float x = bf2f(A.w[b * A.ld_batch + r * A.ld_row + c]);
-  if (A.col_scales) x = bfr(x * A.col_scales[c]);
+  if (A.col_scales) x = bfr(x * A.col_scales[b * A.cs_ld_batch + c]);
   return x;
 }
 
@@ -661,7 +664,7 @@ __global__ void k_quant_generic(GenArgs A, QP p, int out_fmt, int scale_fmt, con
     const int64_t e = brow * A.cols + c;  // dense element index
     if (out_fmt == QZ_OUT_FAKEQUANT) {
       float d = (p.kind == K_INT) ? fakequant_int(p, g, x) : decode(p, g, code);
-      if (A.col_scales) d = bfr(d / A.col_scales[c]);
+      if (A.col_scales) d = bfr(d / A.col_scales[b * A.cs_ld_batch + c]);
       reinterpret_cast<uint16_t*>(q_out)[e] = f2bf(d);
     } else if (out_fmt == QZ_OUT_INT8) {
       reinterpret_cast<int8_t*>(q_out)[e] = (int8_t)((int)code + (int)p.qmin);
@@ -856,7 +859,7 @@ int check_out_fmt(const Plan& pl, int out_fmt) {
 }
 
 GenArgs gen_args(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
-                 const qz_args* a, const Plan& pl, const float* col_scales) {
+                 const qz_args* a, const Plan& pl, const float* col_scales, int64_t cs_ld_batch = 0) {
   GenArgs G;
   G.w = (const uint16_t*)w;
   G.batch = batch; G.rows = rows; G.cols = cols; G.ld_row = ld_row; G.ld_batch = ld_batch;
@@ -865,6 +868,7 @@ GenArgs gen_args(const void* w, int64_t batch, int64_t rows, int64_t cols, int64
   G.bh = a->block_h; G.bw = a->block_w;
   G.ng_item = pl.ng_item;
   G.col_scales = col_scales;
+  G.cs_ld_batch = cs_ld_batch;
   return G;
 }
 
@@ -948,8 +952,8 @@ size_t qz_quantize_workspace_size(int64_t batch, int64_t rows, int64_t cols, con
 
 static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
                          int64_t ld_batch, const qz_args* a, int32_t out_fmt, void* q_out, void* scale_out,
-                         int8_t* zp_out, float* gscale_out, const float* col_scales, void* ws,
-                         size_t ws_bytes, hipStream_t st) {
+                         int8_t* zp_out, float* gscale_out, const float* col_scales, int64_t cs_ld_batch,
+                         void* ws, size_t ws_bytes, hipStream_t st) {
   if (!w || !q_out || !a) return QZ_ERR_NULL;
   if (batch <= 0) return QZ_ERR_SHAPE;
   Plan pl;
@@ -972,7 +976,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
   if (!pl.p.sym && !z_dst) z_dst = W.zp;
   float* gs_dst = gscale_out ? gscale_out : W.gscale;
 
-  GenArgs G = gen_args(w, batch, rows, cols, ld_row, ld_batch, a, pl, col_scales);
+  if (col_scales && cs_ld_batch != 0 && cs_ld_batch < cols) return QZ_ERR_SHAPE;
+  GenArgs G = gen_args(w, batch, rows, cols, ld_row, ld_batch, a, pl, col_scales, cs_ld_batch);
 
   // NVFP4: per-tensor global scale first
   if (pl.kind == K_NV) {
@@ -998,7 +1003,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
   const bool grp = a->strategy == QZ_GROUP || a->strategy == QZ_TENSOR_GROUP;
   const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
   const bool pack_ok = !(pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits != 4 && a->num_bits != 8);
-  const bool al = aligned(w, 16) && aligned(q_out, fq ? 16 : 8) && (!col_scales || aligned(col_scales, 16));
+  const bool al = aligned(w, 16) && aligned(q_out, fq ? 16 : 8) &&
+                  (!col_scales || (aligned(col_scales, 16) && cs_ld_batch % 4 == 0));
   if (grp && pow2 && rows_dense && pack_ok && al && batch <= 65535) {
     FastArgs F;
     F.w = (const uint16_t*)w;
@@ -1014,6 +1020,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.zp_out = z_dst;
     F.gscale = gs_dst;
     F.col_scales = col_scales;
+    F.cs_ld_batch = cs_ld_batch;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const int64_t n_tiles = cdiv(F.units_per_batch, UNROLL * WAVE);
@@ -1049,6 +1056,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       F.zp_out = z_dst;
       F.gscale = gs_dst;
       F.col_scales = nullptr;
+      F.cs_ld_batch = 0;
       TileArgs T;
       T.rows = rows;
       T.tile_rows = th;
@@ -1084,14 +1092,22 @@ int qz_quantize(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_
                 const qz_args* a, int32_t out_fmt, void* q_out, void* scale_out, int8_t* zp_out, float* gscale_out,
                 void* workspace, size_t workspace_bytes, qz_stream_t stream) {
   return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, out_fmt, q_out, scale_out, zp_out, gscale_out,
-                       nullptr, workspace, workspace_bytes, (hipStream_t)stream);
+                       nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,
                       const qz_args* a, const float* col_scales, void* w_out, void* workspace, size_t workspace_bytes,
                       qz_stream_t stream) {
   return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, QZ_OUT_FAKEQUANT, w_out, nullptr, nullptr, nullptr,
-                       col_scales, workspace, workspace_bytes, (hipStream_t)stream);
+                       col_scales, 0, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qz_awq_fake_quant_batched(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row,
+                              int64_t ld_batch, const qz_args* a, const float* col_scales, int64_t cs_ld_batch,
+                              void* w_out, void* workspace, size_t workspace_bytes, qz_stream_t stream) {
+  if (!col_scales) return QZ_ERR_NULL;
+  return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, QZ_OUT_FAKEQUANT, w_out, nullptr, nullptr, nullptr,
+                       col_scales, cs_ld_batch, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 int qz_quantize_qparams(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,

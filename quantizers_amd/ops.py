@@ -183,6 +183,27 @@ def fake_quantize(w: torch.Tensor, a: QuantizationArgs, col_scales: Optional[tor
     return out
 
 
+def fake_quantize_batched(w: torch.Tensor, a: QuantizationArgs, col_scales: torch.Tensor,
+                          out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Q(W_b * s_b) / s_b for a [B, N, K] batch with one scale vector per slice (``col_scales``
+    [B, K]): the batched grid step of per-expert AWQ mappings (qz_awq_fake_quant_batched)."""
+    _check_dev(w, "weight")
+    b, r, c, ld_r, ld_b = _geom(w)
+    cs = col_scales.to(device=w.device, dtype=torch.float32).contiguous()
+    if w.dim() != 3 or cs.shape != (b, c):
+        raise ValueError("fake_quantize_batched: w [B, N, K] and col_scales [B, K]")
+    if out is None:
+        out = torch.empty(w.shape, dtype=torch.bfloat16, device=w.device)
+    ca = a.to_c()
+    lib = _lib.load()
+    ws_n = lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca)) + 4 * b + 256
+    ws = workspace(ws_n, w.device)
+    rc = lib.qz_awq_fake_quant_batched(_ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), _ptr(cs), c, _ptr(out),
+                                       _ptr(ws), ws.numel(), _stream())
+    _lib.check(rc, "qz_awq_fake_quant_batched")
+    return out
+
+
 def observe_minmax(w: torch.Tensor, a: QuantizationArgs) -> Tuple[torch.Tensor, torch.Tensor]:
     _check_dev(w, "weight")
     b, r, c, ld_r, ld_b = _geom(w)
@@ -357,6 +378,21 @@ def awq_grid_scales(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio:
     rc = _lib.load().qz_awq_grid_scales(_ptr(x_mean), _ptr(wm), x_mean.numel(), float(ratio), int(duo_scaling),
                                         _ptr(out), _stream())
     _lib.check(rc, "qz_awq_grid_scales")
+    return out
+
+
+def awq_grid_scales_batched(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo_scaling: bool,
+                            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``awq_grid_scales`` for [B, C] stacks of independent mappings (one launch)."""
+    x_mean = x_mean.to(torch.float32).contiguous()
+    wm = w_mean.to(torch.float32).contiguous() if w_mean is not None else None
+    if x_mean.dim() != 2 or (wm is not None and wm.shape != x_mean.shape):
+        raise ValueError("awq_grid_scales_batched: x_mean / w_mean must be [B, C]")
+    if out is None:
+        out = torch.empty_like(x_mean)
+    rc = _lib.load().qz_awq_grid_scales_batched(_ptr(x_mean), _ptr(wm), x_mean.shape[0], x_mean.shape[1],
+                                                float(ratio), int(duo_scaling), _ptr(out), _stream())
+    _lib.check(rc, "qz_awq_grid_scales_batched")
     return out
 
 

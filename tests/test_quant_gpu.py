@@ -302,3 +302,36 @@ def test_mxfp4_encode_exhaustive_fast_path(cuda, anchor):
     assert torch.all(got["weight_scale"].cpu() == 127)
     ref = ct.compress_weight(w, _oracle_args(a))
     _eq(got["weight_packed"], ref["weight_packed"])
+
+
+@pytest.mark.parametrize("scheme", [SCHEMES[i] for i in (1, 3, 7, 11, 17, 18)], ids=_id)
+def test_batched_col_scales_match_per_slice(cuda, scheme):
+    """qz_awq_fake_quant_batched (one scale vector per slice, the per-expert AWQ grid step) and
+    qz_awq_grid_scales_batched are bit-identical to per-slice calls."""
+    a = QuantizationArgs(**scheme)
+    g = torch.Generator().manual_seed(11)
+    fused = (torch.randn(5, 64, 256, generator=g) * 0.02).to(torch.bfloat16).to(cuda)
+    xm = (torch.rand(5, 256, generator=g) + 0.01).to(cuda)
+    wm = (torch.rand(5, 256, generator=g) + 0.01).to(cuda)
+    for ratio in (0.0, 0.35, 0.95):
+        s = ops.awq_grid_scales_batched(xm, wm, ratio, True)
+        got = ops.fake_quantize_batched(fused, a, s)
+        for e in range(5):
+            s_e = ops.awq_grid_scales(xm[e], wm[e], ratio, True)
+            _eq(s[e].view(torch.int32), s_e.view(torch.int32))
+            _eq(got[e], ops.fake_quantize(fused[e], a, col_scales=s_e))
+
+
+def test_batched_col_scales_expert_shape(cuda):
+    """The per-expert AWQ grid step at a real expert shape (Qwen3-30B-A3B down_proj chunk:
+    16 x [2048, 768], int4 g128): batched launch == per-slice launches."""
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    w = (torch.randn(16, 2048, 768, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    xm = torch.rand(16, 768, device=cuda, generator=g) + 0.01
+    wm = torch.rand(16, 768, device=cuda, generator=g) + 0.01
+    s = ops.awq_grid_scales_batched(xm, wm, 0.5, True)
+    got = ops.fake_quantize_batched(w, a, s)
+    torch.cuda.synchronize()
+    for e in (0, 7, 15):
+        _eq(got[e], ops.fake_quantize(w[e], a, col_scales=s[e].clone()))
