@@ -171,6 +171,18 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
                              int32_t group_size, double* wsum, qz_stream_t stream);
 
 /*
+ * qz_awq_sq_err_accum -- the grid search's loss numerator: *out += sum over [rows, cols] of
+ * f32(bf16(a - b))^2 for two bf16 parent outputs (reference output and the output with the
+ * fake-quantized balance layers), summed in f64 in a fixed order (deterministic).  Replaces
+ * the `(fp16_out - q_out).pow(2).sum()` of [3P] llmcompressor AWQModifier._compute_loss.
+ * workspace: qz_awq_sq_err_workspace_size(rows, cols) bytes.
+ */
+size_t qz_awq_sq_err_workspace_size(int64_t rows, int64_t cols);
+int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols, int64_t lda,
+                        int64_t ldb, double* out, void* workspace, size_t workspace_bytes,
+                        qz_stream_t stream);
+
+/*
  * qz_awq_grid_scales -- one grid point of [3P] AWQModifier._compute_best_scale (fp32):
  * s = clamp(x_mean^r / (w_mean^(1-r) + 1e-4), 1e-4) (duo) or clamp(x_mean^r, 1e-4);
  * s /= sqrt(max(s) * min(s)); inf/nan -> 1.  Single workgroup; channels <= 65536.

@@ -27,7 +27,8 @@ EXPORTS = (
     "qz_observe_minmax", "qz_calculate_qparams", "qz_dequantize", "qz_pack_int32",
     "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_accum",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
-    "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched",
+    "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
+    "qz_awq_sq_err_accum",
 )
 
 
@@ -71,6 +72,8 @@ def load() -> ctypes.CDLL:
         "qz_awq_grid_scales": ([P, P, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "qz_awq_fake_quant": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
         "qz_awq_grid_scales_batched": ([P, P, I64, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
+        "qz_awq_sq_err_workspace_size": ([I64, I64], SZ),
+        "qz_awq_sq_err_accum": ([P, P, I64, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
         "qz_awq_fake_quant_batched": ([P, I64, I64, I64, I64, I64, A, P, I64, P, P, SZ, P], ctypes.c_int),
         "qz_scale_columns": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
         "qz_scale_rows": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),

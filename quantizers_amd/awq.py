@@ -239,13 +239,17 @@ def _run_parent(parent: nn.Module, calls) -> List[torch.Tensor]:
 
 
 def _sq_err(ref: List[torch.Tensor], got: List[torch.Tensor]) -> torch.Tensor:
-    """mean squared error over all calibration outputs, fp64 on the device (no host sync)."""
-    tot = torch.zeros((), dtype=torch.float64, device=ref[0].device)
+    """mean squared error over all calibration outputs, fp64 on the device (no host sync):
+    one fused kernel per output (qz_awq_sq_err_accum) instead of sub / cast / pow / sum."""
+    tot = torch.zeros(1, dtype=torch.float64, device=ref[0].device)
     n = 0
     for a, b in zip(ref, got):
-        tot += (a - b).reshape(-1).float().pow(2).sum().double()
+        if a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16:
+            ops.awq_sq_err_accum(a, b, tot)
+        else:
+            tot += (a - b).reshape(-1).float().pow(2).sum().double()
         n += a.numel()
-    return tot / max(n, 1)
+    return tot[0] / max(n, 1)
 
 
 def _loss(ref: List[torch.Tensor], got: List[torch.Tensor]) -> float:
@@ -479,18 +483,17 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         cols = w2.shape[2]
         xm = torch.empty(len(refs), cols, dtype=torch.float32, device=w2.device)
         wm = torch.empty_like(xm)
+        hs = [torch.cat(h) if len(h) > 1 else h[0] for h in hid]  # all tokens of an expert: [T, I]
+        del hid
         for k, ref in enumerate(refs):
             am = _AbsMean()
-            for t in hid[k]:
-                am.add(t)
+            am.add(hs[k])
             xm[k] = am.mean()
             wsum = torch.zeros(cols, dtype=torch.float64, device=w2.device)
             rows = ops.awq_weight_mean_accum(ref.weight, _group_size_for_mean(a, cols), wsum)
             wm[k] = (wsum / rows).float()
-        # all calibration tokens of an expert in one [T, I] operand: one GEMM per expert and
-        # grid point (2-D GEMMs: the path every other mapping uses)
-        hs = [torch.cat(h) if len(h) > 1 else h[0] for h in hid]
-        del hid
+        # one GEMM per expert and grid point over all its tokens (2-D GEMMs: the path every
+        # other mapping uses)
         w0 = torch.stack([w2[e] for e in es])  # [k, H, I] (pre-search weights)
         ref_out = [nn.functional.linear(h, w0[k]) for k, h in enumerate(hs)]
         n_el = ref_out[0].numel()
@@ -501,7 +504,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
             ops.fake_quantize_batched(w0, a, scales[g], out=wq)
             for k, (h, ro) in enumerate(zip(hs, ref_out)):
-                losses[g, k] = (ro - nn.functional.linear(h, wq[k])).float().pow(2).sum().double()
+                ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq[k]), losses[g, k:k + 1])
         hist = (losses / max(n_el, 1)).cpu()
         out = []
         for k in range(len(refs)):

@@ -59,13 +59,69 @@ __global__ void k_absmean_final(const float* part, int64_t nch, int64_t C, float
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float acc = 0.f;
+#pragma unroll 8
   for (int64_t k = 0; k < nch; ++k) acc += part[k * C + c];
   sum[c] += acc;
 }
 
+// ----------------------------------------------- a5: grid-search loss sum((a - b)^2)
+// [3P] llmcompressor _compute_loss over a parent's outputs: (fp16_out - q_out) in the output
+// dtype (bf16), squared in f32, summed (here in f64, fixed order: deterministic).
+// stage 1: fixed grid, each thread walks 8-element units grid-stride, f64 partial per block
+__device__ __forceinline__ double warp_sum_f64(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+  return v;
+}
+__global__ __launch_bounds__(256) void k_sqdiff_partial(const uint16_t* a, const uint16_t* b, int64_t rows,
+                                                        int64_t cols, int64_t lda, int64_t ldb, int v8,
+                                                        double* part) {
+  double acc = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  if (v8) {  // dense rows (lda == ldb == cols, cols % 8 == 0): flat 16-B units
+    const int64_t n = rows * cols / 8;
+    const uint4* A = reinterpret_cast<const uint4*>(a);
+    const uint4* B = reinterpret_cast<const uint4*>(b);
+    for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < n; u += stride) {
+      const uint4 x = A[u], y = B[u];
+      const uint32_t xa[4] = {x.x, x.y, x.z, x.w}, ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = bfr(__uint_as_float(xa[k] << 16) - __uint_as_float(ya[k] << 16));
+        const float d1 = bfr(__uint_as_float(xa[k] & 0xffff0000u) - __uint_as_float(ya[k] & 0xffff0000u));
+        acc += (double)(d0 * d0);
+        acc += (double)(d1 * d1);
+      }
+    }
+  } else {
+    const int64_t n = rows * cols;
+    for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n; e += stride) {
+      const int64_t r = e / cols, c = e - r * cols;
+      const float d = bfr(bf2f(a[r * lda + c]) - bf2f(b[r * ldb + c]));
+      acc += (double)(d * d);
+    }
+  }
+  acc = warp_sum_f64(acc);
+  __shared__ double red[256 / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+// stage 2: one wave sums the partials in a fixed order and accumulates into *out
+__global__ void k_sqdiff_final(const double* part, int64_t nb, double* out) {
+  double acc = 0.0;
+  for (int64_t k = threadIdx.x; k < nb; k += WAVE) acc += part[k];
+  acc = warp_sum_f64(acc);
+  if (threadIdx.x == 0) *out += acc;
+}
+int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
+  return std::max<int64_t>(1, std::min<int64_t>(2048, cdiv(rows * cols, 256 * 8 * 4)));
+}
+
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
+  // >= 64 tokens per chunk keeps stage 2 short (it is a serial loop over chunks per channel)
   const int64_t bx = cdiv(C, 2048);
-  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 16), cdiv(2048, bx)));
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 64), cdiv(2048, bx)));
   *tc = cdiv(T, nch);
   return cdiv(T, *tc);
 }
@@ -213,6 +269,28 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   int rc = launch_err();
   if (rc) return rc;
   hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 256)), dim3(256), 0, st, part, nch, channels, sum);
+  return launch_err();
+}
+
+size_t qz_awq_sq_err_workspace_size(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)8 * (size_t)sqdiff_blocks(rows, cols);
+}
+
+int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols, int64_t lda, int64_t ldb,
+                        double* out, void* workspace, size_t workspace_bytes, qz_stream_t stream) {
+  if (!a || !b || !out) return QZ_ERR_NULL;
+  if (rows < 0 || cols <= 0 || lda < cols || ldb < cols) return QZ_ERR_SHAPE;
+  if (rows == 0) return QZ_OK;
+  if (!workspace || workspace_bytes < qz_awq_sq_err_workspace_size(rows, cols)) return QZ_ERR_WORKSPACE;
+  const int64_t nb = sqdiff_blocks(rows, cols);
+  const int v8 = lda == cols && ldb == cols && cols % 8 == 0 && aligned(a, 16) && aligned(b, 16);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_sqdiff_partial, dim3((unsigned)nb), dim3(256), 0, st, (const uint16_t*)a, (const uint16_t*)b,
+                     rows, cols, lda, ldb, v8, (double*)workspace);
+  int rc = launch_err();
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_sqdiff_final, dim3(1), dim3(WAVE), 0, st, (const double*)workspace, nb, out);
   return launch_err();
 }
 

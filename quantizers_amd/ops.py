@@ -369,6 +369,29 @@ def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) 
     return r
 
 
+def awq_sq_err_accum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    """out[0] += sum(f32(bf16(a - b))^2) (f64, deterministic): the AWQ grid loss numerator
+    over two bf16 parent outputs of the same shape (qz_awq_sq_err_accum)."""
+    _check_dev(a, "a")
+    if a.shape != b.shape or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise ValueError("awq_sq_err_accum: a and b must be bf16 tensors of the same shape")
+    if out.dtype != torch.float64 or out.numel() < 1 or not out.is_cuda:
+        raise ValueError("awq_sq_err_accum: out must be a float64 device tensor")
+    a2 = a.reshape(-1, a.shape[-1]) if a.dim() != 1 else a.reshape(1, -1)
+    b2 = b.reshape(-1, b.shape[-1]) if b.dim() != 1 else b.reshape(1, -1)
+    if a2.stride(-1) != 1:
+        a2 = a2.contiguous()
+    if b2.stride(-1) != 1:
+        b2 = b2.contiguous()
+    r, c = a2.shape
+    lib = _lib.load()
+    ws = workspace(lib.qz_awq_sq_err_workspace_size(r, c) + 256, a.device)
+    rc = lib.qz_awq_sq_err_accum(_ptr(a2), _ptr(b2), r, c, a2.stride(0), b2.stride(0), _ptr(out), _ptr(ws),
+                                 ws.numel(), _stream())
+    _lib.check(rc, "qz_awq_sq_err_accum")
+    return out
+
+
 def awq_grid_scales(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo_scaling: bool,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
     x_mean = x_mean.to(torch.float32).contiguous()

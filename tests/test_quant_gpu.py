@@ -335,3 +335,20 @@ def test_batched_col_scales_expert_shape(cuda):
     torch.cuda.synchronize()
     for e in (0, 7, 15):
         _eq(got[e], ops.fake_quantize(w[e], a, col_scales=s[e].clone()))
+
+
+@pytest.mark.parametrize("shape,strided", [((4096, 2048), False), ((333, 100), False), ((512, 768), True)])
+def test_awq_sq_err_accum(cuda, shape, strided):
+    """qz_awq_sq_err_accum == sum(f32(bf16(a - b))^2) (f64), dense and strided rows."""
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(*shape, generator=g).to(torch.bfloat16)
+    b = (a.float() + torch.randn(*shape, generator=g) * 0.01).to(torch.bfloat16)
+    want = (a - b).float().pow(2).double().sum().item()
+    ac, bc = a.to(cuda), b.to(cuda)
+    if strided:
+        big = torch.zeros(shape[0], shape[1] + 64, dtype=torch.bfloat16, device=cuda)
+        big[:, :shape[1]] = ac
+        ac = big[:, :shape[1]]
+    out = torch.full((1,), 0.5, dtype=torch.float64, device=cuda)
+    ops.awq_sq_err_accum(ac, bc, out)
+    assert abs(out.item() - 0.5 - want) <= 1e-12 * max(want, 1.0)
