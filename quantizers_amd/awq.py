@@ -228,6 +228,23 @@ def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
     return ei.tokens(i, ref.index[0])
 
 
+def _tokenwise_concat(parent: nn.Module, calls):
+    """A MoE block acts on every token independently (router + experts), so its calibration
+    calls can run as ONE call over all tokens: same per-token math and the same loss sum,
+    one expert loop per grid point instead of one per calibration batch.  Other parents
+    (attention: positions, masks) keep their per-batch calls."""
+    if len(calls) < 2 or not any(is_fused_experts(m) for m in parent.children()):
+        return calls
+    xs = []
+    for args, kwargs in calls:
+        if kwargs or len(args) != 1 or not torch.is_tensor(args[0]) or args[0].dim() != 3 or args[0].shape[0] != 1:
+            return calls
+        xs.append(args[0])
+    if any(x.shape[2] != xs[0].shape[2] for x in xs):
+        return calls
+    return [((torch.cat(xs, dim=1),), {})]
+
+
 def _run_parent(parent: nn.Module, calls) -> List[torch.Tensor]:
     outs = []
     for args, kwargs in calls:
@@ -405,7 +422,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         w_mean = (wsum / rows).float()
         # parent: forward closure over the calibration batches
         if r.parent_kind == "module":
-            calls = caches[r.smooth_name].calls
+            calls = _tokenwise_concat(r.parent, caches[r.smooth_name].calls)
             run: Callable[[], List[torch.Tensor]] = lambda p=r.parent, c=calls: _run_parent(p, c)
         else:
             ei = experts[id(b0.module)]
