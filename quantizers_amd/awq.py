@@ -228,12 +228,23 @@ def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
     return ei.tokens(i, ref.index[0])
 
 
+def _is_tokenwise(m: nn.Module) -> bool:
+    """Parents that act on every token independently: a Linear, a gated MLP, a MoE block
+    (router + fused experts).  Attention and whole decoder layers are not."""
+    if isinstance(m, nn.Linear):
+        return True
+    name = type(m).__name__
+    if name.endswith("MLP") or "SparseMoe" in name or any(is_fused_experts(c) for c in m.children()):
+        return not any("Attention" in type(c).__name__ for c in m.modules())
+    return False
+
+
 def _tokenwise_concat(parent: nn.Module, calls):
-    """A MoE block acts on every token independently (router + experts), so its calibration
-    calls can run as ONE call over all tokens: same per-token math and the same loss sum,
-    one expert loop per grid point instead of one per calibration batch.  Other parents
-    (attention: positions, masks) keep their per-batch calls."""
-    if len(calls) < 2 or not any(is_fused_experts(m) for m in parent.children()):
+    """A token-wise parent (MLP, MoE block, Linear) can run its calibration calls as ONE call
+    over all tokens: same per-token math and the same loss sum, larger GEMMs and one expert
+    loop per grid point instead of one per calibration batch.  Other parents (attention:
+    positions, masks) keep their per-batch calls."""
+    if len(calls) < 2 or not _is_tokenwise(parent):
         return calls
     xs = []
     for args, kwargs in calls:
