@@ -158,7 +158,28 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
     cfg["quantization_config"] = quantization_config(model)
     with open(os.path.join(output_dir, "config.json"), "w") as f:
         json.dump(cfg, f, indent=2, default=str)
+    _write_recipe(getattr(model, "quantization_recipe", None), output_dir)
     return output_dir
+
+
+def _write_recipe(recipe, output_dir: str) -> None:
+    """recipe.yaml beside the checkpoint (llmcompressor's save_pretrained wrapper stores the
+    applied recipe the same way): the recipe file's text, or the dict/YAML text it was given."""
+    import yaml
+    if recipe is None:
+        return
+    path = os.path.join(output_dir, "recipe.yaml")
+    if isinstance(recipe, str):
+        text = open(recipe).read() if os.path.exists(recipe) else recipe
+    elif isinstance(recipe, (dict, list)):
+        try:
+            text = yaml.safe_dump(recipe, sort_keys=False)
+        except yaml.YAMLError:
+            return
+    else:
+        return
+    with open(path, "w") as f:
+        f.write(text)
 
 
 def _load_all(path: str) -> Dict[str, torch.Tensor]:

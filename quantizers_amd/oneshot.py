@@ -157,6 +157,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts)
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
+    model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml
     model.awq_report = report
     if output_dir is not None:
         from .compressor import save_compressed

@@ -124,6 +124,7 @@ def test_awq_int4_g32_end_to_end(cuda, tmp_path):
     sd = compressed_state_dict(m)
     assert _check_against_oracle(m, sd) == 14
     assert os.path.exists(os.path.join(out, "model.safetensors"))
+    assert open(os.path.join(out, "recipe.yaml")).read() == open(recipe).read()
 
 
 def test_awq_layer_matches_oracle_search(cuda):
