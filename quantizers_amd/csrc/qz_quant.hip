@@ -116,6 +116,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef QZ_NT_BYTES
 #define QZ_NT_BYTES (256ll << 20)  // weight bytes per launch above which loads are non-temporal
 #endif
+#ifndef QZ_TILE_NT
+#define QZ_TILE_NT 1  // non-temporal register loads in the tile path above QZ_NT_BYTES
+#endif
 #ifndef QZ_LDS_AUX
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
@@ -413,7 +416,7 @@ struct TileArgs {
   int64_t rows, tile_rows, tile_w8, tiles_c, ld_row;  // tile_w8 = tile width in units
 };
 
-template <int KIND, bool SYM, int MAXU>
+template <int KIND, bool SYM, int MAXU, bool NT = false>
 __global__ __launch_bounds__(BLOCK) void k_tile_fast(FastArgs A, TileArgs T) {
   __shared__ uint32_t red[2][BLOCK / WAVE];
   const int64_t b = blockIdx.y;
@@ -429,7 +432,9 @@ __global__ __launch_bounds__(BLOCK) void k_tile_fast(FastArgs A, TileArgs T) {
     const uint32_t uu = u < U ? u : U - 1;
     const int64_t row = tr * T.tile_rows + uu / (uint32_t)T.tile_w8;
     const int64_t c8 = tc * T.tile_w8 + uu % (uint32_t)T.tile_w8;
-    v[i] = *reinterpret_cast<const uint4*>(wb + row * T.ld_row + c8 * 8);
+    const u32x4* src = reinterpret_cast<const u32x4*>(wb + row * T.ld_row + c8 * 8);
+    const u32x4 t = NT ? __builtin_nontemporal_load(src) : *src;
+    v[i] = make_uint4(t.x, t.y, t.z, t.w);
     oidx[i] = (u < U) ? (b * T.rows + row) * A.units_per_row + c8 : -1;
   }
   QP p = A.p;
@@ -580,7 +585,10 @@ __global__ __launch_bounds__(256) void k_absmax_slices(const uint16_t* w, int64_
   for (; u + 3 * stride < units_per_batch; u += 4 * stride) {
     uint4 v[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = src[u + j * stride];
+    for (int j = 0; j < 4; ++j) {  // read-once stream: non-temporal
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + u + j * stride));
+      v[j] = make_uint4(t.x, t.y, t.z, t.w);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       m = pk_max_u16(m, pk_max_u16(pk_max_u16(v[j].x & 0x7fff7fffu, v[j].y & 0x7fff7fffu),
@@ -741,7 +749,7 @@ using FastFn = void (*)(FastArgs);
 // Infinity Cache: the read-once weight should not evict the outputs; +6 % at 360 MB, -2 % at 90 MB)
 template <int LOGL, int KIND, bool SYM>
 FastFn pick_fq(bool fq, bool nt) {
-  if (fq) return k_group_fast<LOGL, KIND, true, SYM>;
+  if (fq) return nt ? (FastFn)k_group_fast<LOGL, KIND, true, SYM, true> : (FastFn)k_group_fast<LOGL, KIND, true, SYM>;
   return nt ? (FastFn)k_group_fast<LOGL, KIND, false, SYM, true> : (FastFn)k_group_fast<LOGL, KIND, false, SYM>;
 }
 template <int LOGL>
@@ -767,22 +775,26 @@ FastFn pick_fast(int logl, int kind, bool sym, bool fq, bool nt) {
 }
 
 using TileFn = void (*)(FastArgs, TileArgs);
-template <int KIND, bool SYM>
+template <int KIND, bool SYM, bool NT>
 TileFn pick_tile_u(int maxu) {
   switch (maxu) {
-    case 1: return k_tile_fast<KIND, SYM, 1>;
-    case 2: return k_tile_fast<KIND, SYM, 2>;
-    case 4: return k_tile_fast<KIND, SYM, 4>;
-    case 8: return k_tile_fast<KIND, SYM, 8>;
-    default: return k_tile_fast<KIND, SYM, 16>;
+    case 1: return k_tile_fast<KIND, SYM, 1, NT>;
+    case 2: return k_tile_fast<KIND, SYM, 2, NT>;
+    case 4: return k_tile_fast<KIND, SYM, 4, NT>;
+    case 8: return k_tile_fast<KIND, SYM, 8, NT>;
+    default: return k_tile_fast<KIND, SYM, 16, NT>;
   }
 }
-TileFn pick_tile(int kind, bool sym, int maxu) {
+template <bool NT>
+TileFn pick_tile_nt(int kind, bool sym, int maxu) {
   switch (kind) {
-    case K_INT: return sym ? pick_tile_u<K_INT, true>(maxu) : pick_tile_u<K_INT, false>(maxu);
-    case K_FP8: return pick_tile_u<K_FP8, true>(maxu);
-    default: return pick_tile_u<K_FP4, true>(maxu);
+    case K_INT: return sym ? pick_tile_u<K_INT, true, NT>(maxu) : pick_tile_u<K_INT, false, NT>(maxu);
+    case K_FP8: return pick_tile_u<K_FP8, true, NT>(maxu);
+    default: return pick_tile_u<K_FP4, true, NT>(maxu);
   }
+}
+TileFn pick_tile(int kind, bool sym, int maxu, bool nt) {
+  return nt ? pick_tile_nt<true>(kind, sym, maxu) : pick_tile_nt<false>(kind, sym, maxu);
 }
 
 struct Plan {
@@ -1066,7 +1078,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       const int64_t tiles = (rows / th) * (cols / tw);
       int maxu = 1;
       while (maxu * BLOCK < U) maxu *= 2;
-      hipLaunchKernelGGL(pick_tile(pl.kind, pl.p.sym != 0, maxu), dim3((unsigned)tiles, (unsigned)batch), dim3(BLOCK),
+      const bool nt = QZ_TILE_NT && batch * rows * cols * 2 > QZ_NT_BYTES;
+      hipLaunchKernelGGL(pick_tile(pl.kind, pl.p.sym != 0, maxu, nt), dim3((unsigned)tiles, (unsigned)batch), dim3(BLOCK),
                          0, st, F, T);
       return launch_err();
     }

@@ -42,6 +42,11 @@ def main():
         fmt = 2
         codes = torch.empty(ROWS, COLS, dtype=torch.uint8, device=dev)
         scale = torch.empty(ROWS, COLS // G, dtype=torch.bfloat16, device=dev)
+    elif KIND == "fp8block":
+        a = _lib.QzArgs(8, 1, 1, 3, 0, 128, 128, 0)
+        fmt = 2
+        codes = torch.empty(ROWS, COLS, dtype=torch.uint8, device=dev)
+        scale = torch.empty(ROWS // 128, COLS // 128, dtype=torch.bfloat16, device=dev)
     else:  # mx
         a = _lib.QzArgs(4, 1, 1, 2, 32, 0, 0, 3)
         fmt = 3
@@ -99,6 +104,8 @@ def main():
         d = sorted(s.elapsed_time(e) * 1e3 for s, e in ev)
         print(f"{name:28s} median {d[K//2]:7.2f} us  -> {nbytes / (d[K//2] * 1e-6) / 1e9:7.0f} GB/s")
     alg = ROWS * COLS * 2 + ROWS * COLS * BITS // 8 + ROWS * COLS // G * 2
+    if KIND in ("fp8", "fp8block"):
+        alg = ROWS * COLS * 3 + (ROWS * COLS // (G if KIND == "fp8" else 16384)) * 2
     for p in paths:
         v = sorted(res[p])
         print(f"{os.path.basename(p):28s} median {v[len(v)//2]:7.2f} us  min {v[0]:7.2f} us  "
