@@ -116,6 +116,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef QZ_NT_BYTES
 #define QZ_NT_BYTES (256ll << 20)  // weight bytes per launch above which loads are non-temporal
 #endif
+#ifndef QZ_NT_STORES
+#define QZ_NT_STORES 1  // non-temporal output stores in the NT (large-launch) group path
+#endif
 #ifndef QZ_TILE_NT
 #define QZ_TILE_NT 1  // non-temporal register loads in the tile path above QZ_NT_BYTES
 #endif
@@ -132,9 +135,26 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
   return r;
 }
 
+// output stores; NTS = non-temporal (streaming outputs of launches far larger than the MALL)
+template <bool NTS, typename T>
+__device__ __forceinline__ void st_out(T* p, const T v) {
+  if constexpr (NTS) {
+    if constexpr (sizeof(T) == 4) {
+      __builtin_nontemporal_store(__builtin_bit_cast(uint32_t, v), reinterpret_cast<uint32_t*>(p));
+    } else if constexpr (sizeof(T) == 8) {
+      typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x2_t, v), reinterpret_cast<u32x2_t*>(p));
+    } else {
+      __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(p));
+    }
+  } else {
+    *p = v;
+  }
+}
+
 // quotient, round/clamp/encode and store of one 8-element unit whose group params are known.
 // unit = dense output unit index.  Returns false for invalid (out-of-range) units.
-template <int KIND, bool FQ, bool SYM>
+template <int KIND, bool FQ, bool SYM, bool NTS = false>
 __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, const GP& g, const f32x2* x,
                                              const f32x2* cs, const int64_t unit) {
 
@@ -159,7 +179,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       }
       word |= (pk & 0xffu) << (8 * k);
     }
-    reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
+    st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, word);
     return;
   }
 
@@ -207,7 +227,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         for (int k = 0; k < 4; ++k) { d[2 * k] = bfr(d[2 * k] / cs[k].x); d[2 * k + 1] = bfr(d[2 * k + 1] / cs[k].y); }
       }
       uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
-      reinterpret_cast<uint4*>(A.q_out)[unit] = o;
+      st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, o);
     } else if (A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
       // word = sum_i (0x4B000000 + u_i) << 4i  - 0xFB000000   (mod 2^32): one shift-add per code
       uint32_t acc = 0u;
@@ -216,7 +236,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         acc += __float_as_uint(q[k].x) << (8 * k);
         acc += __float_as_uint(q[k].y) << (8 * k + 4);
       }
-      reinterpret_cast<uint32_t*>(A.q_out)[unit] = acc - 0xFB000000u;
+      st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, acc - 0xFB000000u);
     } else {
       uint32_t c[8];
 #pragma unroll
@@ -225,14 +245,14 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         c[2 * k + 1] = __float_as_uint(q[k].y) & 0xffu;
       }
       if (A.out_fmt == QZ_OUT_PACKED_INT32) {  // 8 bits: u = q + 128, 4 per word
-        reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
-                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+        st_out<NTS>(reinterpret_cast<uint2*>(A.q_out) + unit, make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24)));
       } else {  // int8 (signed) bytes
         const uint32_t off = (uint32_t)(-(int)p.qmin);
 #pragma unroll
         for (int i = 0; i < 8; ++i) c[i] = (c[i] - off) & 0xffu;
-        reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
-                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+        st_out<NTS>(reinterpret_cast<uint2*>(A.q_out) + unit, make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                             c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24)));
       }
     }
   } else {
@@ -271,21 +291,21 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         if (A.col_scales) d[i] = bfr(d[i] / ((i & 1) ? cs[i >> 1].y : cs[i >> 1].x));
       }
       uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
-      reinterpret_cast<uint4*>(A.q_out)[unit] = o;
+      st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, o);
     } else if (KIND == K_FP8) {
-      reinterpret_cast<uint2*>(A.q_out)[unit] = make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
-                                                           c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24));
+      st_out<NTS>(reinterpret_cast<uint2*>(A.q_out) + unit, make_uint2(c[0] | (c[1] << 8) | (c[2] << 16) | (c[3] << 24),
+                                                           c[4] | (c[5] << 8) | (c[6] << 16) | (c[7] << 24)));
     } else {  // fp4 packed: element 2k in the low nibble of byte k
       uint32_t word = 0;
 #pragma unroll
       for (int i = 0; i < 8; ++i) word |= c[i] << (4 * i);
-      reinterpret_cast<uint32_t*>(A.q_out)[unit] = word;
+      st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, word);
     }
   }
 }
 
 // Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
-template <int LOGL, int KIND, bool FQ, bool SYM>
+template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS = false>
 __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
                                              const bool valid, const float gs, const int lane, const int64_t b) {
   constexpr int L = 1 << LOGL;
@@ -341,7 +361,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   ps.sym = SYM;
   const GP g = group_params(ps, mn, mx, gs);
   if (!valid) return;
-  encode_store<KIND, FQ, SYM>(A, ps, g, x, cs, unit);
+  encode_store<KIND, FQ, SYM, NTS>(A, ps, g, x, cs, unit);
   if ((lane & (L - 1)) == 0) {
     const int64_t gi = unit >> LOGL;
     if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
@@ -350,7 +370,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
 }
 
-template <int LOGL, int KIND, bool FQ, bool SYM>
+template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS = false>
 __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t b, int64_t tile,
                                              int lane) {
   const float gs = (KIND == K_NV) ? A.gscale[b] : 0.f;
@@ -366,7 +386,7 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
       if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
     }
 #else
-    process_unit<LOGL, KIND, FQ, SYM>(A, p, v[u], unit, valid, gs, lane, b);
+    process_unit<LOGL, KIND, FQ, SYM, NTS>(A, p, v[u], unit, valid, gs, lane, b);
 #endif
   }
 }
@@ -403,7 +423,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
   uint4 v[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
-  process_tile<LOGL, KIND, FQ, SYM>(A, p, v, b, tile, lane);
+  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES>(A, p, v, b, tile, lane);
 }
 
 // --------------------------------------------------------------- single-pass tile path

@@ -352,3 +352,26 @@ def test_awq_sq_err_accum(cuda, shape, strided):
     out = torch.full((1,), 0.5, dtype=torch.float64, device=cuda)
     ops.awq_sq_err_accum(ac, bc, out)
     assert abs(out.item() - 0.5 - want) <= 1e-12 * max(want, 1.0)
+
+
+@pytest.mark.parametrize("scheme", [SCHEMES[i] for i in (0, 3, 11, 15, 17, 18)], ids=_id)
+def test_large_launch_nontemporal_path(cuda, scheme):
+    """Launches above 256 MiB take the non-temporal load/store variants (group, tile and NVFP4
+    absmax kernels): one [9, 4096, 4096] launch == nine per-slice launches (which take the
+    oracle-checked default path)."""
+    a = QuantizationArgs(**scheme)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    w = (torch.randn(9, 4096, 4096, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    assert w.numel() * 2 > 256 << 20
+    big = ops.compress_weight(w, a)
+    for e in (0, 4, 8):
+        one = ops.compress_weight(w[e], a)
+        for k, v in one.items():
+            if k == "weight_shape":
+                continue
+            gv = big[k][e] if big[k].dim() > 1 or k != "weight_global_scale" else big[k][e:e + 1]
+            _eq(gv.reshape(v.shape), v)
+    if not a.is_nvfp4:  # AWQ fake-quant with column scales, non-temporal variant
+        s = torch.rand(4096, device=cuda, generator=g) + 0.5
+        fq = ops.fake_quantize(w, a, col_scales=s)
+        _eq(fq[5], ops.fake_quantize(w[5], a, col_scales=s))
