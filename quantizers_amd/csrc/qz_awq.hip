@@ -25,25 +25,43 @@ int launch_err() {
 }
 
 // ---------------------------------------------------------- a3: sum_t |x[t, c]|
-// stage 1: block (256 threads) = 256 channel octets x one token chunk -> partial[chunk][c]
+// stage 1: block = 4 waves over 512 channels (lane = 8 channels, one 16-B load) x a chunk of tc
+// tokens; wave w takes tokens w, w+4, ... (4 independent loads in flight per lane), the 4 wave
+// sums are added in a fixed order through LDS -> partial[chunk][c]
 __global__ __launch_bounds__(256) void k_absmean_partial_v8(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
                                                             int64_t tc, float* part) {
-  const int64_t c8 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c8 * 8 >= C) return;
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 512 + lane * 8;
+  const bool in = c0 < C;
   const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t t = t0; t < t1; ++t) {
-    const uint4 v = *reinterpret_cast<const uint4*>(x + t * ld + c8 * 8);
+  auto add = [&](const uint4 v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       acc[2 * k] += fabsf(__uint_as_float(w[k] << 16));
       acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
     }
+  };
+  if (in) {
+    int64_t t = t0 + wv;
+    for (; t + 12 < t1; t += 16) {
+      uint4 v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const uint4*>(x + (t + 4 * j) * ld + c0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) add(v[j]);
+    }
+    for (; t < t1; t += 4) add(*reinterpret_cast<const uint4*>(x + t * ld + c0));
   }
-  float* dst = part + (int64_t)blockIdx.y * C + c8 * 8;
-  *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += 256) {
+    const int64_t c = (int64_t)blockIdx.x * 512 + j;
+    if (c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
+  }
 }
 __global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
                                                             int64_t tc, float* part) {
@@ -54,14 +72,20 @@ __global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, i
   for (int64_t t = t0; t < t1; ++t) acc += fabsf(bf2f(x[t * ld + c]));
   part[(int64_t)blockIdx.y * C + c] = acc;
 }
-// stage 2: fixed-order sum over chunks, accumulated into sum[c]
-__global__ void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
-  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// stage 2: block = 64 channels x 4 chunk lanes; lane sums chunks w, w+4, ... (fixed order),
+// the 4 lane sums are added in a fixed order; accumulated into sum[c]
+__global__ __launch_bounds__(256) void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   float acc = 0.f;
-#pragma unroll 8
-  for (int64_t k = 0; k < nch; ++k) acc += part[k * C + c];
-  sum[c] += acc;
+  if (c < C) {
+#pragma unroll 4
+    for (int64_t k = wv; k < nch; k += 4) acc += part[k * C + c];
+  }
+  red[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && c < C) sum[c] += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // ----------------------------------------------- a5: grid-search loss sum((a - b)^2)
@@ -119,8 +143,8 @@ int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
 }
 
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
-  // >= 64 tokens per chunk keeps stage 2 short (it is a serial loop over chunks per channel)
-  const int64_t bx = cdiv(C, 2048);
+  // >= 64 tokens per chunk (16 per wave); about 2048 stage-1 blocks in total
+  const int64_t bx = cdiv(C, 512);
   int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 64), cdiv(2048, bx)));
   *tc = cdiv(T, nch);
   return cdiv(T, *tc);
@@ -135,28 +159,31 @@ __global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, 
   __shared__ double red[4][512];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * 512 + lane * 8;
-  const bool in = c0 < C;
+  const bool in = c0 < C;  // uniform per group of L lanes (C % group == 0)
   const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t r = r0 + wv; r < r1; r += 4) {
-    uint4 v = in ? *reinterpret_cast<const uint4*>(w + r * ld + c0) : make_uint4(0, 0, 0, 0);
-    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
-    float a[8];
+  auto row = [&](const uint4 v) {
+    const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
+    // group absmax on |bf16| bit patterns (v_pk_max_u16 + DPP), then |w| / bf16(amax + 1e-6)
+    const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
+    const float m = __uint_as_float(grp_max_u<L>(max(pm & 0xffffu, pm >> 16)) << 16);
+    const float d = bfr(m + 1e-6f);
+    const float rd = __builtin_amdgcn_rcpf(d);  // bf16(|w| * rcp(d)) == bf16(|w| / d): rcp lemma
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      a[2 * k] = fabsf(__uint_as_float(u[k] << 16));
-      a[2 * k + 1] = fabsf(__uint_as_float(u[k] & 0xffff0000u));
+      acc[2 * k] += (double)bfr(__uint_as_float(u[k] << 16) * rd);
+      acc[2 * k + 1] += (double)bfr(__uint_as_float(u[k] & 0xffff0000u) * rd);
     }
-    float m = a[0];
+  };
+  int64_t r = r0 + wv;
+  for (; r + 12 < r1; r += 16) {  // 4 rows in flight per lane
+    uint4 v[4];
 #pragma unroll
-    for (int i = 1; i < 8; ++i) m = fmaxf(m, a[i]);
+    for (int j = 0; j < 4; ++j) v[j] = in ? *reinterpret_cast<const uint4*>(w + (r + 4 * j) * ld + c0) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int s = 1; s < L; s <<= 1) m = fmaxf(m, __shfl_xor(m, s, WAVE));
-    const float d = bfr(m + 1e-6f);  // amax + 1e-6 in bf16
-    const float rd = __builtin_amdgcn_rcpf(d);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] += (double)bfr(a[i] * rd);  // bf16(|w| / d)
+    for (int j = 0; j < 4; ++j) row(v[j]);
   }
+  for (; r < r1; r += 4) row(in ? *reinterpret_cast<const uint4*>(w + r * ld + c0) : make_uint4(0, 0, 0, 0));
 #pragma unroll
   for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
   __syncthreads();
@@ -237,6 +264,38 @@ __global__ void k_scale_rows(uint16_t* w, int64_t R, int64_t C, int64_t ld, cons
   *p = f2bf(divide ? x / s[r] : x * s[r]);
 }
 
+// 8 bf16 per thread (one 16-B access), grid (column octets, rows); column scales as 2 float4
+template <bool COLS>
+__global__ __launch_bounds__(256) void k_scale_v8(uint16_t* w, int64_t R, int64_t C, int64_t ld, const float* s,
+                                                  int divide) {
+  const int64_t c8 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c8 * 8 >= C) return;
+  float cs[8];
+  if (COLS) {
+    const float4 a = *reinterpret_cast<const float4*>(s + c8 * 8);
+    const float4 b = *reinterpret_cast<const float4*>(s + c8 * 8 + 4);
+    cs[0] = a.x; cs[1] = a.y; cs[2] = a.z; cs[3] = a.w; cs[4] = b.x; cs[5] = b.y; cs[6] = b.z; cs[7] = b.w;
+  }
+  for (int64_t r = blockIdx.y; r < R; r += gridDim.y) {
+    uint4* p = reinterpret_cast<uint4*>(w + r * ld + c8 * 8);
+    const uint4 v = *p;
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float x0 = __uint_as_float(u[k] << 16), x1 = __uint_as_float(u[k] & 0xffff0000u);
+      const float s0 = COLS ? cs[2 * k] : s[r], s1 = COLS ? cs[2 * k + 1] : s[r];
+      const float y0 = divide ? x0 / s0 : x0 * s0, y1 = divide ? x1 / s1 : x1 * s1;
+      o[k] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
+    }
+    *p = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+bool v8_ok(const void* w, int64_t C, int64_t ld, const float* s, bool cols) {
+  return C % 8 == 0 && ld % 8 == 0 && aligned(w, 16) && (!cols || aligned(s, 16));
+}
+
 }  // namespace
 
 extern "C" {
@@ -260,7 +319,7 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   float* part = (float*)workspace;
   const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16);
   if (v8) {
-    dim3 grid((unsigned)cdiv(channels / 8, 256), (unsigned)nch);
+    dim3 grid((unsigned)cdiv(channels, 512), (unsigned)nch);
     hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(256), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
   } else {
     dim3 grid((unsigned)cdiv(channels, 256), (unsigned)nch);
@@ -268,7 +327,7 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   }
   int rc = launch_err();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 256)), dim3(256), 0, st, part, nch, channels, sum);
+  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 64)), dim3(256), 0, st, part, nch, channels, sum);
   return launch_err();
 }
 
@@ -348,6 +407,12 @@ int qz_scale_columns(void* w, int64_t rows, int64_t cols, int64_t ld, const floa
                      qz_stream_t stream) {
   if (!w || !s) return QZ_ERR_NULL;
   if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
+  if (v8_ok(w, cols, ld, s, true)) {
+    dim3 grid((unsigned)cdiv(cols / 8, 256), (unsigned)std::min<int64_t>(rows, 65535));
+    hipLaunchKernelGGL(k_scale_v8<true>, grid, dim3(256), 0, (hipStream_t)stream, (uint16_t*)w, rows, cols, ld, s,
+                       (int)divide);
+    return launch_err();
+  }
   hipLaunchKernelGGL(k_scale_cols, dim3((unsigned)cdiv(rows * cols, 256)), dim3(256), 0, (hipStream_t)stream,
                      (uint16_t*)w, rows, cols, ld, s, (int)divide);
   return launch_err();
@@ -357,6 +422,12 @@ int qz_scale_rows(void* w, int64_t rows, int64_t cols, int64_t ld, const float* 
                   qz_stream_t stream) {
   if (!w || !s) return QZ_ERR_NULL;
   if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
+  if (v8_ok(w, cols, ld, s, false)) {
+    dim3 grid((unsigned)cdiv(cols / 8, 256), (unsigned)std::min<int64_t>(rows, 65535));
+    hipLaunchKernelGGL(k_scale_v8<false>, grid, dim3(256), 0, (hipStream_t)stream, (uint16_t*)w, rows, cols, ld, s,
+                       (int)divide);
+    return launch_err();
+  }
   hipLaunchKernelGGL(k_scale_rows, dim3((unsigned)cdiv(rows * cols, 256)), dim3(256), 0, (hipStream_t)stream,
                      (uint16_t*)w, rows, cols, ld, s, (int)divide);
   return launch_err();

@@ -121,6 +121,42 @@ __device__ __forceinline__ float bf16_quot(float a, float b, float rb) {
   return bfr(q);
 }
 
+// ------------------------------------------------------- cross-lane integer reductions
+// xor-butterfly reduction over groups of L consecutive lanes.  L <= 16 uses DPP (VALU
+// cross-lane, no LDS round trip): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
+// row_mirror; wider groups fall back to ds_bpermute shuffles.  Reductions run on uint32 keys
+// (order-preserving images of the floats) so no NaN canonicalisation is needed and the DPP
+// move folds into v_max_u32_dpp / v_min_u32_dpp.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);  // full EXEC: every source lane valid
+}
+template <int L>
+__device__ __forceinline__ uint32_t grp_max_u(uint32_t v) {
+  if (L >= 2) v = max(v, dpp<0xB1>(v));
+  if (L >= 4) v = max(v, dpp<0x4E>(v));
+  if (L >= 8) v = max(v, dpp<0x141>(v));
+  if (L >= 16) v = max(v, dpp<0x140>(v));
+#pragma unroll
+  for (int m = 16; m < L; m <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 64));
+  return v;
+}
+template <int L>
+__device__ __forceinline__ uint32_t grp_min_u(uint32_t v) {
+  if (L >= 2) v = min(v, dpp<0xB1>(v));
+  if (L >= 4) v = min(v, dpp<0x4E>(v));
+  if (L >= 8) v = min(v, dpp<0x141>(v));
+  if (L >= 16) v = min(v, dpp<0x140>(v));
+#pragma unroll
+  for (int m = 16; m < L; m <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, 64));
+  return v;
+}
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
+}
+
+
 // ------------------------------------------------------------- per-group params
 struct GP {
   float s;      // dense scale (bf16 value, 2^k for MX, f32 for NV)

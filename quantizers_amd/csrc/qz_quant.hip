@@ -39,35 +39,6 @@ __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
-// xor-butterfly reduction over groups of L consecutive lanes.  L <= 16 uses DPP (VALU
-// cross-lane, no LDS round trip): quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
-// row_mirror; wider groups fall back to ds_bpermute shuffles.  Reductions run on uint32 keys
-// (order-preserving images of the floats) so no NaN canonicalisation is needed and the DPP
-// move folds into v_max_u32_dpp / v_min_u32_dpp.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);  // full EXEC: every source lane valid
-}
-template <int L>
-__device__ __forceinline__ uint32_t grp_max_u(uint32_t v) {
-  if (L >= 2) v = max(v, dpp<0xB1>(v));
-  if (L >= 4) v = max(v, dpp<0x4E>(v));
-  if (L >= 8) v = max(v, dpp<0x141>(v));
-  if (L >= 16) v = max(v, dpp<0x140>(v));
-#pragma unroll
-  for (int m = 16; m < L; m <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, WAVE));
-  return v;
-}
-template <int L>
-__device__ __forceinline__ uint32_t grp_min_u(uint32_t v) {
-  if (L >= 2) v = min(v, dpp<0xB1>(v));
-  if (L >= 4) v = min(v, dpp<0x4E>(v));
-  if (L >= 8) v = min(v, dpp<0x141>(v));
-  if (L >= 16) v = min(v, dpp<0x140>(v));
-#pragma unroll
-  for (int m = 16; m < L; m <<= 1) v = min(v, (uint32_t)__shfl_xor((int)v, m, WAVE));
-  return v;
-}
 // float helpers for the generic path
 template <int L>
 __device__ __forceinline__ float grp_max(float v) {
@@ -81,11 +52,6 @@ __device__ __forceinline__ float grp_min(float v) {
   for (int m = 1; m < L; m <<= 1) v = fminf(v, __shfl_xor(v, m, WAVE));
   return v;
 }
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
-  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
-}
-
 struct FastArgs {
   const uint16_t* w;
   int64_t n_units;          // batch*rows*cols/8
@@ -133,6 +99,17 @@ __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
   r.x = __uint_as_float(u << 16);
   r.y = __uint_as_float(u & 0xffff0000u);
   return r;
+}
+
+// bf16(d / c) for a bf16 value d and an f32 divisor c (AWQ's Q(W*s)/s): q = d * rcp(c) is
+// within 2 ulps of the quotient, so bf16(q) is the answer unless q lies within 4 ulps of a bf16
+// rounding midpoint (low 16 bits near 0x8000), where the IEEE division decides.
+__device__ __forceinline__ float bf16_div(float d, float c) {
+  const float q = d * __builtin_amdgcn_rcpf(c);
+  const uint32_t b = __float_as_uint(q);
+  if (__builtin_expect((((b & 0xffffu) + 4u - 0x8000u) & 0xffffu) < 8u || !(fabsf(c) >= 0x1.0p-100f && fabsf(c) <= 0x1.0p+100f), 0))
+    return bfr(d / c);
+  return bfr(q);
 }
 
 // output stores; NTS = non-temporal (streaming outputs of launches far larger than the MALL)
@@ -224,7 +201,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       }
       if (A.col_scales) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { d[2 * k] = bfr(d[2 * k] / cs[k].x); d[2 * k + 1] = bfr(d[2 * k + 1] / cs[k].y); }
+        for (int k = 0; k < 4; ++k) { d[2 * k] = bf16_div(d[2 * k], cs[k].x); d[2 * k + 1] = bf16_div(d[2 * k + 1], cs[k].y); }
       }
       uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
       st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, o);
@@ -288,7 +265,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         d[i] = decode(p, g, c[i]);
-        if (A.col_scales) d[i] = bfr(d[i] / ((i & 1) ? cs[i >> 1].y : cs[i >> 1].x));
+        if (A.col_scales) d[i] = bf16_div(d[i], (i & 1) ? cs[i >> 1].y : cs[i >> 1].x);
       }
       uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
       st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, o);
