@@ -375,3 +375,31 @@ def test_large_launch_nontemporal_path(cuda, scheme):
         s = torch.rand(4096, device=cuda, generator=g) + 0.5
         fq = ops.fake_quantize(w, a, col_scales=s)
         _eq(fq[5], ops.fake_quantize(w[5], a, col_scales=s))
+
+
+FULL = [dict(num_bits=4, type="int", symmetric=False, group_size=128),
+        dict(num_bits=4, type="int", symmetric=True, group_size=32),
+        dict(num_bits=8, type="float", group_size=32),
+        dict(num_bits=8, type="float", strategy="block", block_structure=[128, 128]),
+        dict(num_bits=4, type="float", group_size=32, scale_dtype="uint8"),
+        dict(num_bits=4, type="float", strategy="tensor_group", group_size=16, scale_dtype="float8_e4m3fn")]
+
+
+@pytest.mark.parametrize("scheme", FULL, ids=_id)
+def test_full_size_parity_c_oracle(cuda, scheme):
+    """BASELINE shape [11008, 4096] (with 0.1 % x20 outliers and an all-zero group row):
+    every on-disk tensor bit-identical to the plain-C oracle (oracle/quant_ref.c)."""
+    import qref
+    a = QuantizationArgs(**scheme)
+    g = torch.Generator().manual_seed(21)
+    w = torch.randn(11008, 4096, generator=g) * 0.02
+    mask = torch.rand(11008, 4096, generator=g) < 1e-3
+    w[mask] *= 20
+    w[5, :256] = 0.0  # all-zero groups (D1)
+    w = w.to(torch.bfloat16)
+    want = qref.compress_weight(w, _oracle_args(a))
+    got = ops.compress_weight(w.to(cuda), a)
+    want = {k: v for k, v in want.items() if not k.startswith("_")}
+    assert set(got) == set(want), (set(got), set(want))
+    for k, v in want.items():
+        _eq(got[k], v)
