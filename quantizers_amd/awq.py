@@ -280,10 +280,6 @@ def _sq_err(ref: List[torch.Tensor], got: List[torch.Tensor]) -> torch.Tensor:
     return tot[0] / max(n, 1)
 
 
-def _loss(ref: List[torch.Tensor], got: List[torch.Tensor]) -> float:
-    return _sq_err(ref, got).item()
-
-
 def _group_size_for_mean(a: QuantizationArgs, cols: int) -> int:
     if a.strategy in ("group", "tensor_group"):
         return a.group_size

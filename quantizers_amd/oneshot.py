@@ -21,8 +21,8 @@ import torch
 from torch import nn
 
 from . import awq as awq_mod
-from .model import LinearRef, checkpoint_name, decoder_layers, iter_linears, model_type
-from .quantization import QuantizationArgs, QuantizationScheme
+from .model import checkpoint_name, decoder_layers, iter_linears, model_type
+from .quantization import QuantizationScheme
 from .recipe import AWQModifier, QuantizationModifier, match_any, parse_recipe
 
 log = logging.getLogger(__name__)
