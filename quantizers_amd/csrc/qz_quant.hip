@@ -129,6 +129,23 @@ __device__ __forceinline__ void st_out(T* p, const T v) {
   }
 }
 
+// two f32 -> packed bf16 pair (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pk_bf16(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+// packed bf16(d / c) for a pair: bf16_div's rcp path on both lanes, the IEEE division for a
+// pair with a quotient near a bf16 midpoint
+__device__ __forceinline__ uint32_t bf16_div_pk(f32x2 d, f32x2 c) {
+  const f32x2 r = {__builtin_amdgcn_rcpf(c.x), __builtin_amdgcn_rcpf(c.y)};
+  const f32x2 q = d * r;
+  const uint32_t bx = __float_as_uint(q.x), by = __float_as_uint(q.y);
+  const bool near = ((((bx & 0xffffu) + 4u - 0x8000u) & 0xffffu) < 8u) | ((((by & 0xffffu) + 4u - 0x8000u) & 0xffffu) < 8u);
+  const bool range = (fabsf(c.x) >= 0x1.0p-100f) & (fabsf(c.x) <= 0x1.0p+100f) & (fabsf(c.y) >= 0x1.0p-100f) &
+                     (fabsf(c.y) <= 0x1.0p+100f);
+  if (__builtin_expect(near || !range, 0)) return pk_bf16(f32x2{d.x / c.x, d.y / c.y});
+  return pk_bf16(q);
+}
+
 // quotient, round/clamp/encode and store of one 8-element unit whose group params are known.
 // unit = dense output unit index.  Returns false for invalid (out-of-range) units.
 template <int KIND, bool FQ, bool SYM, bool NTS = false>
@@ -192,19 +209,17 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       q[k] = tk + mg;
     }
     if (FQ) {
-      float d[8];
+      // pairwise: bf16(bf16(round(t) - zp) * s) [/ col scale], the last bf16 rounding packs the
+      // output word directly (round() keeps the sign of zero: -0 dequantizes to -0)
+      const f32x2 s2 = {g.s, g.s};
+      uint32_t o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        // round() keeps the sign of zero (-0 dequantizes to -0)
-        d[2 * k] = bfr(bfr(__builtin_rintf(t[k].x) - g.zp) * g.s);
-        d[2 * k + 1] = bfr(bfr(__builtin_rintf(t[k].y) - g.zp) * g.s);
+        const f32x2 r = {__builtin_rintf(t[k].x), __builtin_rintf(t[k].y)};
+        const f32x2 dq = bfr2(bfr2(r - zp2) * s2);
+        o[k] = A.col_scales ? bf16_div_pk(dq, cs[k]) : pk_bf16(dq);
       }
-      if (A.col_scales) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) { d[2 * k] = bf16_div(d[2 * k], cs[k].x); d[2 * k + 1] = bf16_div(d[2 * k + 1], cs[k].y); }
-      }
-      uint4 o = make_uint4(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]), pack2bf(d[4], d[5]), pack2bf(d[6], d[7]));
-      st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, o);
+      st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, make_uint4(o[0], o[1], o[2], o[3]));
     } else if (A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
       // word = sum_i (0x4B000000 + u_i) << 4i  - 0xFB000000   (mod 2^32): one shift-add per code
       uint32_t acc = 0u;
@@ -284,7 +299,8 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
 // Process one 8-element unit: observe (group reduce over L lanes), qparams, quantize, store.
 template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS = false>
 __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, const uint4 v, const int64_t unit,
-                                             const bool valid, const float gs, const int lane, const int64_t b) {
+                                             const bool valid, const float gs, const int lane, const int64_t b,
+                                             const f32x2* cs_in) {
   constexpr int L = 1 << LOGL;
   // unit: dense output index (batch*units_per_batch + local); valid is uniform within a group
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
@@ -295,15 +311,12 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
     x[k].y = __uint_as_float(wd[k] & 0xffff0000u);
   }
   f32x2 cs[4];
-  if (FQ && A.col_scales) {
-    const float* cs_b = A.col_scales + b * A.cs_ld_batch;
-    const int64_t c0 = (unit % A.units_per_row) * 8;
-    const float4 c_lo = *reinterpret_cast<const float4*>(cs_b + c0);
-    const float4 c_hi = *reinterpret_cast<const float4*>(cs_b + c0 + 4);
-    cs[0] = f32x2{c_lo.x, c_lo.y}; cs[1] = f32x2{c_lo.z, c_lo.w};
-    cs[2] = f32x2{c_hi.x, c_hi.y}; cs[3] = f32x2{c_hi.z, c_hi.w};
+  if (FQ && A.col_scales) {  // column scales were fetched with the tile (k_group_fast)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = bfr2(x[k] * cs[k]);  // W * s in the weight dtype
+    for (int k = 0; k < 4; ++k) {
+      cs[k] = cs_in[k];
+      x[k] = bfr2(x[k] * cs[k]);  // W * s in the weight dtype
+    }
   }
 
   // ---- observe: memoryless min/max over the group (exact in bf16), on integer keys
@@ -349,7 +362,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
 
 template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS = false>
 __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t b, int64_t tile,
-                                             int lane) {
+                                             int lane, const f32x2 (*csu)[4]) {
   const float gs = (KIND == K_NV) ? A.gscale[b] : 0.f;
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
@@ -363,7 +376,7 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
       if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
     }
 #else
-    process_unit<LOGL, KIND, FQ, SYM, NTS>(A, p, v[u], unit, valid, gs, lane, b);
+    process_unit<LOGL, KIND, FQ, SYM, NTS>(A, p, v[u], unit, valid, gs, lane, b, csu[u]);
 #endif
   }
 }
@@ -394,13 +407,29 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
                                      (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
                                      NT ? 2 : QZ_LDS_AUX);
   }
+  // AWQ fake-quant: fetch this lane's column scales while the DMA is in flight
+  f32x2 csu[UNROLL][4];
+  if (FQ && A.col_scales) {
+    const float* cs_b = A.col_scales + b * A.cs_ld_batch;
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+      unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
+      const int64_t c0 = (A.units_per_batch < (int64_t)1 << 32 ? (int64_t)((uint32_t)unit % (uint32_t)A.units_per_row)
+                                                                  : unit % A.units_per_row) * 8;
+      const float4 c_lo = *reinterpret_cast<const float4*>(cs_b + c0);
+      const float4 c_hi = *reinterpret_cast<const float4*>(cs_b + c0 + 4);
+      csu[u][0] = f32x2{c_lo.x, c_lo.y}; csu[u][1] = f32x2{c_lo.z, c_lo.w};
+      csu[u][2] = f32x2{c_hi.x, c_hi.y}; csu[u][3] = f32x2{c_hi.z, c_hi.w};
+    }
+  }
   QP p = A.p;
   p.kind = KIND;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
   uint4 v[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
-  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES>(A, p, v, b, tile, lane);
+  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES>(A, p, v, b, tile, lane, csu);
 }
 
 // --------------------------------------------------------------- single-pass tile path
