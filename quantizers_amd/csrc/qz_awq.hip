@@ -46,6 +46,13 @@ __global__ __launch_bounds__(256) void k_absmean_partial_v8(const uint16_t* x, i
   };
   if (in) {
     int64_t t = t0 + wv;
+    for (; t + 28 < t1; t += 32) {  // 8 token loads in flight per lane
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const uint4*>(x + (t + 4 * j) * ld + c0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) add(v[j]);
+    }
     for (; t + 12 < t1; t += 16) {
       uint4 v[4];
 #pragma unroll
@@ -143,9 +150,9 @@ int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
 }
 
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
-  // >= 64 tokens per chunk (16 per wave); about 2048 stage-1 blocks in total
+  // >= 128 tokens per chunk (32 per wave: one round of 8 loads); about 2048 stage-1 blocks
   const int64_t bx = cdiv(C, 512);
-  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 64), cdiv(2048, bx)));
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 128), cdiv(2048, bx)));
   *tc = cdiv(T, nch);
   return cdiv(T, *tc);
 }
