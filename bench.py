@@ -179,7 +179,7 @@ def minimax_pass(ops, QuantizationArgs, dev, gen, world, rank):
         dist.barrier()
     t = torch.tensor([(time.perf_counter() - t0) / reps], device=dev, dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _all_reduce_max(t)
     t = t.item()
     p_exp = n_layers * n_exp * 3 * inter * hid
     p_att = n_layers * sum(r * c for r, c in attn)
@@ -188,6 +188,24 @@ def minimax_pass(ops, QuantizationArgs, dev, gen, world, rank):
     return {"params": p_exp + p_att, "ms": t * 1e3, "params_per_s": (p_exp + p_att) / t, "ranks": world,
             "alg_GBps": (p_exp * (2 + 0.5 + 2 / 32) + p_att * (2 + 1 + 2 / 32)) / t / 1e9,
             "sharding": "layers round-robin over ranks (strong scaling)"}
+
+
+def _all_reduce_max(t):
+    if dist.get_backend() == "gloo" and t.is_cuda:
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.MAX)
+        t.copy_(h)
+    else:
+        _all_reduce_max(t)
+
+
+def _all_gather_into(out, inp):
+    if dist.get_backend() == "gloo":
+        parts = [torch.empty_like(inp, device="cpu") for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, inp.cpu())
+        out.copy_(torch.stack(parts))
+    else:
+        dist.all_gather_into_tensor(out, inp)
 
 
 def _event_us(fn, n, stream):
@@ -246,9 +264,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # QZ_BENCH_BACKEND=gloo: rehearsal of the multi-rank code path on a box with fewer GPUs than
+    # ranks (ranks share devices, collectives go through host memory); the driver's N-GPU runs
+    # use the default RCCL ("nccl") backend, one rank per GPU.
+    backend = os.environ.get("QZ_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -289,7 +316,7 @@ def main():
     el = time.perf_counter() - t0
     t = torch.tensor([el], device=dev, dtype=torch.float64)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _all_reduce_max(t)
     el = t.item()
 
     # ---- per-launch kernel duration with HIP events on the launch stream (roofline)
@@ -320,15 +347,15 @@ def main():
         gathered_codes = torch.empty((world,) + tuple(bufs["codes"].shape), dtype=bufs["codes"].dtype, device=dev)
         gathered_scale = torch.empty((world,) + tuple(bufs["scale"].shape), dtype=bufs["scale"].dtype, device=dev)
         for _ in range(3):
-            dist.all_gather_into_tensor(gathered_codes, bufs["codes"])
-            dist.all_gather_into_tensor(gathered_scale, bufs["scale"])
+            _all_gather_into(gathered_codes, bufs["codes"])
+            _all_gather_into(gathered_scale, bufs["scale"])
         torch.cuda.synchronize()
         dist.barrier()
         ta = time.perf_counter()
         reps = 10
         for _ in range(reps):
-            dist.all_gather_into_tensor(gathered_codes, bufs["codes"])
-            dist.all_gather_into_tensor(gathered_scale, bufs["scale"])
+            _all_gather_into(gathered_codes, bufs["codes"])
+            _all_gather_into(gathered_scale, bufs["scale"])
         torch.cuda.synchronize()
         allgather = (time.perf_counter() - ta) / reps * 1e3
 
