@@ -342,3 +342,42 @@ def test_expert_awq_sharded_two_ranks(cuda, tmp_path):
     for k, v in m.state_dict().items():
         _eq(v, two[k], k)
     assert len(m.awq_report["model.layers.0"]) == 9
+
+
+def test_moe_norm_to_all_experts_matches_oracle(cuda):
+    """post_attention_layernorm -> every expert's w1/w3 (parent = the MoE block): the scales
+    applied (from x_mean over the MoE block input and w_mean over all 2E balance slices) and
+    the smoothing of the norm and of every expert slice vs a CPU restatement."""
+    from quantizers_amd.awq import awq_layer
+    from quantizers_amd.recipe import AWQMapping
+    from quantizers_amd.quantization import QuantizationArgs
+    from quantizers_amd.oneshot import _capture_layer0_inputs, _batches
+    m = _minimax(layers=1, experts=4).to(cuda)
+    layer = m.model.layers[0]
+    experts = layer.mlp.experts
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    pre = "model.layers.0.block_sparse_moe.experts"
+    quantized = {f"{pre}.{e}.{p}": a for e in range(4) for p in ("w1", "w2", "w3")}
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(_calib(n=3, s=40, vocab=256), None, None, cuda))
+    seen = []
+    h = layer.mlp.register_forward_pre_hook(lambda mod, args: seen.append(args[0].detach().clone()))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    norm0 = layer.post_attention_layernorm.weight.detach().cpu().clone()
+    gu0 = experts.gate_up_proj.detach().cpu().clone()
+    rep = awq_layer(layer, "model.layers.0", inputs,
+                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*w1$", "re:.*w3$"])], quantized,
+                    mtype="minimax_m2")
+    r = rep["model.layers.0.post_attention_layernorm"]
+    assert len(r["balance"]) == 8 and r["parent"] == "model.layers.0.block_sparse_moe"
+    s_ref, n_ref = None, 0
+    for x in seen:
+        (s_ref, n_ref) = ct.awq_accumulate_mean(x.cpu(), None if s_ref is None else (s_ref, n_ref))
+    x_mean = s_ref / n_ref
+    w_mean = ct.awq_layer_means([gu0[e, :64] for e in range(4)] + [gu0[e, 64:] for e in range(4)],
+                                ct.QArgs(group_size=32))
+    s = ct.awq_grid_scales(x_mean, w_mean, r["best_ratio"], True)
+    _eq(layer.post_attention_layernorm.weight, (norm0.float() / s).to(torch.bfloat16), "norm smoothed")
+    _eq(experts.gate_up_proj.data, (gu0.float() * s.view(1, 1, -1)).to(torch.bfloat16), "w1/w3 smoothed")
