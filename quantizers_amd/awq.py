@@ -325,6 +325,24 @@ def _independent_batches(resolved: List[ResolvedMapping]) -> List[List[ResolvedM
     return out
 
 
+def _grid_ranks(enabled: bool) -> Tuple[int, int]:
+    """(world, rank) for splitting a mapping's grid ratios, (1, 0) when not distributed."""
+    import torch.distributed as dist
+    if not enabled or not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
+
+
+def _all_reduce_sum(t: torch.Tensor) -> None:
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo" and t.is_cuda:  # gloo: host staging
+        h = t.cpu()
+        dist.all_reduce(h)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t)
+
+
 def _sharded_search(batch: List[ResolvedMapping], search_chunk, chunk: int = 1) -> List[Any]:
     """Run ``search_chunk`` (a list of mappings -> a list of results) over consecutive chunks of
     a batch of independent mappings; under torch.distributed rank r takes chunks r, r + world,
@@ -405,8 +423,9 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         ei.snapshot()
     n_batches = len(layer_inputs)
 
-    def search(r: ResolvedMapping):
-        """Grid search of one mapping; returns (best_ratio, best_loss, history, best_scales) or None."""
+    def search(r: ResolvedMapping, grid_shard: bool = False):
+        """Grid search of one mapping; returns (best_ratio, best_loss, history, best_scales) or None.
+        ``grid_shard``: split the grid ratios over the ranks (all ranks run this mapping)."""
         b0 = r.balance[0]
         if b0.index is None:
             x_mean = stats[r.smooth_name].mean()
@@ -448,12 +467,16 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                         outs.append(nn.functional.linear(mod.act_fn(gate) * up, mod.down_proj[e]))
                     return outs
         ref_out = run()
-        # 3. grid search: losses stay on the device
+        # 3. grid search: losses stay on the device.  Under torch.distributed (and outside a
+        # sharded batch of mappings) the ratios are split over the ranks: rank r
+        # evaluates ratios r, r + world, ...; the loss vector is summed over ranks (every other
+        # entry is an exact 0), so every rank sees the bit-identical history of one process
         orig = [_view(g).clone() for g in groups]
         tmp = [torch.empty_like(o) for o in orig]
         scales = torch.empty_like(x_mean)
-        losses = []
-        for i in range(n_grid):
+        world, rank = _grid_ranks(grid_shard)
+        losses = torch.zeros(n_grid, dtype=torch.float64, device=x_mean.device)
+        for i in range(rank, n_grid, world):
             ratio = i / n_grid
             ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
             for g, w0, t in zip(groups, orig, tmp):
@@ -462,10 +485,12 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                 else:
                     ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
                     _view(g).copy_(t)
-            losses.append(_sq_err(ref_out, run()))
+            losses[i] = _sq_err(ref_out, run())
         for g, w0 in zip(groups, orig):
             _view(g).copy_(w0)
-        history = torch.stack(losses).cpu().tolist()
+        if world > 1:
+            _all_reduce_sum(losses)
+        history = losses.cpu().tolist()
         finite = [(l, i) for i, l in enumerate(history) if l == l]
         if not finite:
             raise RuntimeError(f"AWQ: no finite loss for {r.smooth_name} (history {history})")
@@ -543,7 +568,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     report: Dict[str, Any] = {}
     for batch in _independent_batches(resolved):
         if len(batch) == 1:
-            apply(batch[0], search(batch[0]))
+            apply(batch[0], search(batch[0], grid_shard=True))
             continue
         # mutually independent single-layer-parent mappings (e.g. every expert's w3 -> w2):
         # search all (sharded over ranks under torch.distributed), then smooth in order

@@ -381,3 +381,33 @@ def test_moe_norm_to_all_experts_matches_oracle(cuda):
     s = ct.awq_grid_scales(x_mean, w_mean, r["best_ratio"], True)
     _eq(layer.post_attention_layernorm.weight, (norm0.float() / s).to(torch.bfloat16), "norm smoothed")
     _eq(experts.gate_up_proj.data, (gu0.float() * s.view(1, 1, -1)).to(torch.bfloat16), "w1/w3 smoothed")
+
+
+def _awq_rank_dense(rank, world, port, out):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m = _qwen3().to("cuda:0")
+        oneshot(m, os.path.join(ROOT, "configs/recipes/awq_w4a16_g32.yaml"), dataset=_calib(), max_seq_length=64)
+        if rank == world - 1:
+            torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dense_awq_grid_split_three_ranks(cuda, tmp_path):
+    """Dense AWQ with the 20 grid ratios split over 3 ranks (gloo control plane, one card):
+    bit-identical smoothed model to the one-process run."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "rank2.pt")
+    mp.spawn(_awq_rank_dense, args=(3, port, out), nprocs=3, join=True)
+    m = _qwen3().to(cuda)
+    oneshot(m, os.path.join(ROOT, "configs/recipes/awq_w4a16_g32.yaml"), dataset=_calib(), max_seq_length=64)
+    other = torch.load(out, weights_only=True)
+    for k, v in m.state_dict().items():
+        _eq(v, other[k], k)
