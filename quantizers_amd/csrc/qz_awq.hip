@@ -138,12 +138,17 @@ __global__ __launch_bounds__(256) void k_sqdiff_partial(const uint16_t* a, const
   __syncthreads();
   if (threadIdx.x == 0) part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
-// stage 2: one wave sums the partials in a fixed order and accumulates into *out
-__global__ void k_sqdiff_final(const double* part, int64_t nb, double* out) {
+// stage 2: one workgroup (4 waves) sums the partials in a fixed order (thread t: t, t+256, ...;
+// then wave sums; then the 4 wave sums in order) and accumulates into *out
+__global__ __launch_bounds__(256) void k_sqdiff_final(const double* part, int64_t nb, double* out) {
   double acc = 0.0;
-  for (int64_t k = threadIdx.x; k < nb; k += WAVE) acc += part[k];
+#pragma unroll 4
+  for (int64_t k = threadIdx.x; k < nb; k += 256) acc += part[k];
   acc = warp_sum_f64(acc);
-  if (threadIdx.x == 0) *out += acc;
+  __shared__ double red[256 / WAVE];
+  if ((threadIdx.x & (WAVE - 1)) == 0) red[threadIdx.x / WAVE] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) *out += ((red[0] + red[1]) + red[2]) + red[3];
 }
 int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
   return std::max<int64_t>(1, std::min<int64_t>(2048, cdiv(rows * cols, 256 * 8 * 4)));
@@ -356,7 +361,7 @@ int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols
                      rows, cols, lda, ldb, v8, (double*)workspace);
   int rc = launch_err();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_sqdiff_final, dim3(1), dim3(WAVE), 0, st, (const double*)workspace, nb, out);
+  hipLaunchKernelGGL(k_sqdiff_final, dim3(1), dim3(256), 0, st, (const double*)workspace, nb, out);
   return launch_err();
 }
 
