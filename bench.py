@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-model-pass", action="store_true")
+    p.add_argument("--python-loop", action="store_true",
+                   help="one Python qz_quantize call per step instead of one qz_quantize_many call")
     p.add_argument("--graph", action="store_true",
                    help="replay the K steps as one captured hipGraph (measured slower, see DESIGN.md §6)")
     p.add_argument("--profile-only", action="store_true",
@@ -315,9 +317,17 @@ def main():
         graph.replay()  # untimed: first replay uploads the graph
         torch.cuda.synchronize()
 
+    # Default: the K steps go through qz_quantize_many -- one host call that enqueues the K
+    # qz_quantize launches (one per step, each over its own resident copy) -- so the ~20 us
+    # Python/ctypes cost per call cannot leave the GPU idle between the ~21 us kernels.
+    many = None if (graph is not None or args.python_loop) else \
+        prep.prepare_many([copies[i % args.copies] for i in range(args.steps)])
+
     def run_steps():
         if graph is not None:
             graph.replay()
+        elif many is not None:
+            many(stream)
         else:
             for i in range(args.steps):
                 step(i)
@@ -451,7 +461,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": KERNEL_NAME, "kernel_ms_mean": k_ms_mean,
                          "kernel_timing": "HIP events around the K back-to-back launches of the timed region / K"
-                                          + (" (one hipGraph replay)" if graph is not None else ""),
+                                          + (" (one hipGraph replay)" if graph is not None else
+                                             " (one qz_quantize_many call)" if many is not None else
+                                             " (Python loop of qz_quantize calls)"),
                          "kernel_ms_per_launch_events_mean": k_ms_each_mean,
                          "kernel_ms_per_launch_events_median": k_ms_each_med,
                          "alg_bytes_per_launch": ALG_BYTES, "traffic_source": tsrc},

@@ -102,6 +102,21 @@ int qz_quantize(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_
                 size_t workspace_bytes, qz_stream_t stream);
 
 /*
+ * qz_quantize_many -- qz_quantize over n independent weights of one shape and one scheme (e.g.
+ * the same projection of every layer), one launch per weight, enqueued in order on `stream`
+ * from a single host call.  Replaces the compressor's per-module loop over targeted Linears
+ * (save_pretrained(save_compressed=True), do_oneshot.py:197) for callers that hold many
+ * same-shape weights; each item is exactly a qz_quantize call.  w / q_out / scale_out are
+ * arrays of n device pointers; zp_out / gscale_out may be NULL (no item needs them) or arrays
+ * of n pointers.  The workspace is reused by every item (stream order).  Returns the first
+ * non-zero status (items before it are enqueued).
+ */
+int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* const* scale_out,
+                     int8_t* const* zp_out, float* const* gscale_out, int64_t batch, int64_t rows,
+                     int64_t cols, int64_t ld_row, int64_t ld_batch, const qz_args* a,
+                     int32_t out_fmt, void* workspace, size_t workspace_bytes, qz_stream_t stream);
+
+/*
  * qz_quantize_qparams -- quantize with caller-supplied qparams (stateful observers such as the
  * recipes' `minmax`, recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:48).  Replaces [3P]
  * compressed-tensors quantize(x, scale, zero_point, args) / fake_quantize(...).

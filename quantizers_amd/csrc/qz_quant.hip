@@ -88,6 +88,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #ifndef QZ_TILE_NT
 #define QZ_TILE_NT 1  // non-temporal register loads in the tile path above QZ_NT_BYTES
 #endif
+#ifndef QZ_REG_LOADS
+#define QZ_REG_LOADS 0
+#endif
 #ifndef QZ_LDS_AUX
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
@@ -399,6 +402,16 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
   if (tile >= tiles) return;
   const int64_t b = blockIdx.y;
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
+#if QZ_REG_LOADS  // tuning knob: direct-to-register 16-B loads instead of the LDS-DMA staging
+  uint4 v[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
+    if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + unit)));
+    else v[u] = src[unit];
+  }
+#else
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
     int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
@@ -407,6 +420,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
                                      (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
                                      NT ? 2 : QZ_LDS_AUX);
   }
+#endif
   // AWQ fake-quant: fetch this lane's column scales while the DMA is in flight
   f32x2 csu[UNROLL][4];
   if (FQ && A.col_scales) {
@@ -425,10 +439,12 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
   }
   QP p = A.p;
   p.kind = KIND;
+#if !QZ_REG_LOADS
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
   uint4 v[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
+#endif
   process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES>(A, p, v, b, tile, lane, csu);
 }
 
@@ -1132,6 +1148,21 @@ int qz_quantize(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_
                 void* workspace, size_t workspace_bytes, qz_stream_t stream) {
   return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, out_fmt, q_out, scale_out, zp_out, gscale_out,
                        nullptr, 0, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* const* scale_out,
+                     int8_t* const* zp_out, float* const* gscale_out, int64_t batch, int64_t rows, int64_t cols,
+                     int64_t ld_row, int64_t ld_batch, const qz_args* a, int32_t out_fmt, void* workspace,
+                     size_t workspace_bytes, qz_stream_t stream) {
+  if (n < 0) return QZ_ERR_SHAPE;
+  if (n > 0 && (!w || !q_out || !scale_out)) return QZ_ERR_NULL;
+  for (int64_t i = 0; i < n; ++i) {  // one launch per weight, in order on the stream
+    const int rc = quantize_impl(w[i], batch, rows, cols, ld_row, ld_batch, a, out_fmt, q_out[i], scale_out[i],
+                                 zp_out ? zp_out[i] : nullptr, gscale_out ? gscale_out[i] : nullptr, nullptr, 0,
+                                 workspace, workspace_bytes, (hipStream_t)stream);
+    if (rc) return rc;
+  }
+  return QZ_OK;
 }
 
 int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,

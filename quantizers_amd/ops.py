@@ -23,7 +23,7 @@ slices ``[E, N, K]`` (fused MoE experts).  There is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, Optional, Tuple
+from typing import Callable, Dict, Optional, Sequence, Tuple
 
 import torch
 
@@ -471,6 +471,32 @@ class PreparedQuantize:
         rc = self.lib.qz_quantize(_P(w.data_ptr()), b, r, c, ld_r, ld_b, *self._args_tail, st)
         if rc:
             _lib.check(rc, "qz_quantize")
+
+    def prepare_many(self, ws: Sequence[torch.Tensor]) -> Callable[..., None]:
+        """Marshal a qz_quantize_many call over every weight of ``ws`` (same geometry as
+        ``w_like``) into the prepared outputs; the returned ``go(stream=None)`` enqueues one
+        launch per weight from ONE host call."""
+        b, r, c, ld_r, ld_b = self.geom
+        for w in ws:
+            if _geom(w) != self.geom or not w.is_cuda:
+                raise ValueError("prepare_many: every weight needs the prepared geometry and a device")
+        n = len(ws)
+
+        def arr(t):
+            return None if t is None else (ctypes.c_void_p * n)(*([t.data_ptr()] * n))
+
+        args = (n, (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws]), arr(self.out["codes"]),
+                arr(self.out["scale"]), arr(self.out.get("zero_point")), arr(self.out.get("global_scale")),
+                b, r, c, ld_r, ld_b, ctypes.byref(self.ca), self.out_fmt, _P(self.ws.data_ptr()), self.ws.numel())
+        keep = list(ws)  # the pointers stay valid while the closure lives
+
+        def go(stream=None) -> None:
+            st = _P(stream.cuda_stream) if stream is not None else _stream()
+            rc = self.lib.qz_quantize_many(*args, st)
+            if rc:
+                _lib.check(rc, "qz_quantize_many")
+        go.weights = keep
+        return go
 
 
 def unpack_zero_points(packed: torch.Tensor, num_bits: int, shape) -> torch.Tensor:

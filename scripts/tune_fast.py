@@ -73,20 +73,19 @@ def main():
             same = torch.equal(ref[0], cur[0]) and torch.equal(ref[1].view(torch.int16), cur[1].view(torch.int16))
             if not same:
                 print(f"NOTE: {lib._name} output differs from {paths[0]} (expected only for probe builds)")
-    K = 60
+    K = int(os.environ.get("K", 60))
     res = {p: [] for p in paths}
-    for rnd in range(8):
+    for rnd in range(int(os.environ.get("ROUNDS", 8))):
         for p, lib in zip(paths, libs):
             for i in range(10):
                 run(lib, i)
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-            for i in range(K):
-                ev[i][0].record(st)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for i in range(K):  # back-to-back launches, one event pair around the region
                 run(lib, i)
-                ev[i][1].record(st)
+            e1.record(st)
             torch.cuda.synchronize()
-            d = sorted(s.elapsed_time(e) * 1e3 for s, e in ev)
-            res[p].append(d[K // 2])
+            res[p].append(e0.elapsed_time(e1) * 1e3 / K)
     # reference points: torch copy (read+write 2x90 MB) and a read-only sum over one copy
     src = ws[0]
     dst = torch.empty_like(src)
@@ -95,14 +94,14 @@ def main():
                               src.numel() * 2)]:
         for i in range(10):
             fn(i)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
         for i in range(K):
-            ev[i][0].record(st)
             fn(i)
-            ev[i][1].record(st)
+        e1.record(st)
         torch.cuda.synchronize()
-        d = sorted(s.elapsed_time(e) * 1e3 for s, e in ev)
-        print(f"{name:28s} median {d[K//2]:7.2f} us  -> {nbytes / (d[K//2] * 1e-6) / 1e9:7.0f} GB/s")
+        d = [e0.elapsed_time(e1) * 1e3 / K] * (K + 1)
+        print(f"{name:28s} mean   {d[K//2]:7.2f} us  -> {nbytes / (d[K//2] * 1e-6) / 1e9:7.0f} GB/s")
     alg = ROWS * COLS * 2 + ROWS * COLS * BITS // 8 + ROWS * COLS // G * 2
     if KIND in ("fp8", "fp8block"):
         alg = ROWS * COLS * 3 + (ROWS * COLS // (G if KIND == "fp8" else 16384)) * 2

@@ -403,3 +403,36 @@ def test_full_size_parity_c_oracle(cuda, scheme):
     assert set(got) == set(want), (set(got), set(want))
     for k, v in want.items():
         _eq(got[k], v)
+
+
+def test_quantize_many_equals_single_calls(cuda):
+    """qz_quantize_many (one host call, one launch per weight) == qz_quantize per weight, with
+    distinct output buffers per item; and the bench's prepare_many (shared outputs) leaves the
+    last weight's result."""
+    import ctypes
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    ws = [_edge_weight(96, 1024, 128, seed=s).to(cuda) for s in range(3)]
+    ref = [ops.compress_weight(w, a) for w in ws]
+    outs = [ops.quantize_weight(torch.zeros_like(w), a) for w in ws]
+    lib = _lib.load()
+    n = len(ws)
+    arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+    ca = a.to_c()
+    nb = lib.qz_quantize_workspace_size(1, 96, 1024, ctypes.byref(ca))
+    wsp = torch.empty(max(nb, 256), dtype=torch.uint8, device=cuda)
+    rc = lib.qz_quantize_many(n, arr(ws), arr([o["codes"] for o in outs]), arr([o["scale"] for o in outs]), None,
+                              None, 1, 96, 1024, 1024, 96 * 1024, ctypes.byref(ca), ops.default_out_fmt(a),
+                              ctypes.c_void_p(wsp.data_ptr()), wsp.numel(),
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    for o, r in zip(outs, ref):
+        assert torch.equal(o["codes"].cpu(), r["weight_packed"].cpu())
+        assert torch.equal(o["scale"].cpu().view(torch.int16), r["weight_scale"].cpu().view(torch.int16))
+    assert lib.qz_quantize_many(-1, None, None, None, None, None, 1, 96, 1024, 1024, 96 * 1024, ctypes.byref(ca),
+                                0, None, 0, None) == _lib.QZ_ERR_SHAPE
+    prep = ops.PreparedQuantize(ws[0], a, {"codes": outs[0]["codes"], "scale": outs[0]["scale"],
+                                           "zero_point": outs[0]["zero_point"]})
+    prep.prepare_many(ws)()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0]["codes"].cpu(), ref[-1]["weight_packed"].cpu())
