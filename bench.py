@@ -70,11 +70,19 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(seconds: float):
+def cpu_baseline(seconds: float, measured=None):
     """The oracle's torch-op restatement of compressed-tensors (oracle/ct_torch.py), timed on the
-    host cores on the same synthetic weight."""
+    host cores on the same synthetic weight.  The oracle is used only here (the
+    CPU leg): besides the timing it checks the GPU's measured output slice ``measured`` =
+    (input rows, packed codes, scales) bit for bit against the plain-C restatement."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ct_torch as ct  # CPU baseline leg only
+    import qref  # checker only
+    ok = None
+    if measured is not None:
+        w_in, codes, scale = measured
+        ref_p, ref_s = qref.int_sym_group_pack(w_in, BITS, GROUP)
+        ok = bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
 
     threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
     torch.set_num_threads(threads)
@@ -89,10 +97,11 @@ def cpu_baseline(seconds: float):
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 3) or n >= 1000:
             break
-    return {"value": n * PARAMS / el, "unit": "params/s", "cores": threads, "kind": "port",
+    res = {"value": n * PARAMS / el, "unit": "params/s", "cores": threads, "kind": "port",
             "sample": f"oracle/ct_torch.compress_weight (compressed-tensors op sequence, torch CPU) on the same "
                       f"bf16 [{ROWS},{COLS}] int4-g{GROUP} weight, {n} calls in {el:.1f}s, "
                       f"torch threads={threads}, os.cpu_count()={os.cpu_count()}, cpu='{cpu_model()}'"}
+    return res, ok
 
 
 def _timed(fn, reps=3):
@@ -370,15 +379,11 @@ def main():
     k_ms_each_mean = sum(durs) / len(durs)
     k_ms_each_med = durs[len(durs) // 2]
 
-    # ---- correctness guard on the measured buffers (bit-exact vs the C oracle on a slice)
-    ok = None
+    # ---- the measured buffers' first 256 rows, checked against the oracle in the CPU leg below
+    measured = None
     if rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import qref  # checker only
         last = (args.steps - 1) % args.copies
-        ref_p, ref_s = qref.int_sym_group_pack(copies[last][:256].cpu(), BITS, GROUP)
-        ok = bool(torch.equal(bufs["codes"][:256].cpu(), ref_p) and
-                  torch.equal(bufs["scale"][:256].cpu().view(torch.int16), ref_s.view(torch.int16)))
+        measured = (copies[last][:256].cpu(), bufs["codes"][:256].cpu(), bufs["scale"][:256].cpu())
 
     # ---- reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
     allgather = None
@@ -430,9 +435,9 @@ def main():
         other = other_configs(ops, QuantizationArgs, dev, gen)
         other["minimax_m2_1_mixedprec_sharded"] = minimax_pass(ops, QuantizationArgs, dev, gen, world, rank)
 
-    cpu = None
+    cpu, ok = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
+        cpu, ok = cpu_baseline(args.cpu_seconds, measured)
 
     if rank == 0:
         ms_step = el / args.steps * 1e3
