@@ -261,6 +261,36 @@ def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream):
     return res
 
 
+def awq_oneshot_layers(dev, n_layers=2, n_seq=16, seq=2048):
+    """BASELINE.json configs[1] end to end on a truncated model: Qwen3-4B (public dims, random
+    bf16 weights: no checkpoint offline) with ``n_layers`` decoder layers, the AWQ int4-g128
+    recipe, ``n_seq`` x ``seq`` random calibration tokens, through ``quantizers_amd.oneshot``
+    (capture layer-0 inputs, per layer: activation statistics, 20-point grid search with the
+    fused fake-quant kernel and the parent forwards, smoothing, propagation)."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+    from quantizers_amd.oneshot import oneshot
+    cfg = AutoConfig.from_pretrained(os.path.join(ROOT, "configs", "models", "qwen3-4b"))
+    cfg.num_hidden_layers = n_layers
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    g = torch.Generator().manual_seed(42)
+    data = [{"input_ids": torch.randint(0, cfg.vocab_size, (seq,), generator=g)} for _ in range(n_seq)]
+    recipe = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g128.yaml")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    oneshot(model=model, recipe=recipe, dataset=data, max_seq_length=seq, num_calibration_samples=n_seq, device=dev)
+    torch.cuda.synchronize()
+    t = time.perf_counter() - t0
+    rep = model.awq_report
+    n_map = sum(len(v) for v in rep.values())
+    del model
+    torch.cuda.empty_cache()
+    return {"model": "Qwen3-4B dims, random bf16 weights", "layers": n_layers, "calibration_tokens": n_seq * seq,
+            "mappings": n_map, "s_total": t, "s_per_layer": t / n_layers,
+            "projected_36_layers_s": t / n_layers * 36, "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
+
+
 def read_pmc_traffic():
     """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -429,6 +459,11 @@ def main():
         model_pass = {"params": nparams, "ms": mp * 1e3, "params_per_s": nparams / mp,
                       "alg_GBps": nparams * (2 + BITS / 8 + 2 / GROUP) / mp / 1e9, "launches": len(ws)}
 
+    # ---- AWQ oneshot (scale search + smoothing) on a 2-layer Qwen3-4B, BASELINE configs[1]
+    awq_e2e = None
+    if not args.no_model_pass and world == 1:
+        awq_e2e = awq_oneshot_layers(dev)
+
     # ---- the other BASELINE configs, one whole-model pass each (reported beside the headline)
     other = None
     if not args.no_model_pass:
@@ -477,6 +512,7 @@ def main():
             "allgather_ms": allgather,
             "qwen3_4b_all_linears": model_pass,
             "awq_kernels": awq,
+            "awq_oneshot_qwen3_4b": awq_e2e,
             "other_configs": other,
         }
         print(json.dumps(line), flush=True)
