@@ -256,6 +256,56 @@ def _tokenwise_concat(parent: nn.Module, calls):
     return [((torch.cat(xs, dim=1),), {})]
 
 
+def _same(a, b) -> bool:
+    """Structural equality of two cached call arguments (tensors by value)."""
+    if torch.is_tensor(a) or torch.is_tensor(b):
+        return torch.is_tensor(a) and torch.is_tensor(b) and a.shape == b.shape and a.dtype == b.dtype and \
+            a.device == b.device and (a is b or torch.equal(a, b))
+    if isinstance(a, (tuple, list)) or isinstance(b, (tuple, list)):
+        return type(a) is type(b) and len(a) == len(b) and all(_same(x, y) for x, y in zip(a, b))
+    if isinstance(a, dict) or isinstance(b, dict):
+        return isinstance(a, dict) and isinstance(b, dict) and a.keys() == b.keys() and \
+            all(_same(a[k], b[k]) for k in a)
+    return a is b or (type(a) is type(b) and a == b)
+
+
+def _batchwise_concat(calls, max_tokens: int = 1 << 17):
+    """A non-token-wise parent (self-attention) whose calibration calls differ only in their
+    ``hidden_states`` (every sample the same length, the same positions / rotary embeddings /
+    mask, all with batch 1) runs them as calls over up to ``max_tokens`` tokens stacked along
+    the batch dimension: the per-sequence attention is unchanged (the mask and the position
+    embeddings broadcast over the batch), the loss sums the same elements, and there are ~16x
+    fewer launches and larger GEMM / attention kernels per grid point."""
+    if len(calls) < 2:
+        return calls
+
+    def hidden(call):
+        args, kwargs = call
+        if args:
+            return args[0] if len(args) == 1 and "hidden_states" not in kwargs else None
+        return kwargs.get("hidden_states")
+
+    hs = [hidden(c) for c in calls]
+    if any(h is None or not torch.is_tensor(h) or h.dim() != 3 or h.shape[0] != 1 or h.shape != hs[0].shape
+           for h in hs):
+        return calls
+    args0, kw0 = calls[0]
+    rest0 = {k: v for k, v in kw0.items() if k != "hidden_states"}
+    for args, kwargs in calls[1:]:
+        if bool(args) != bool(args0) or not _same(rest0, {k: v for k, v in kwargs.items() if k != "hidden_states"}):
+            return calls
+    for v in rest0.values():  # batch-1 tensors must broadcast: only leading dims of size 1
+        for t in (v if isinstance(v, (tuple, list)) else (v,)):
+            if torch.is_tensor(t) and t.dim() >= 3 and t.shape[0] != 1:
+                return calls
+    per = max(1, max_tokens // hs[0].shape[1])
+    out = []
+    for i in range(0, len(hs), per):
+        h = torch.cat(hs[i:i + per], dim=0)
+        out.append(((h,), dict(rest0)) if args0 else ((), dict(rest0, hidden_states=h)))
+    return out
+
+
 def _run_parent(parent: nn.Module, calls) -> List[torch.Tensor]:
     outs = []
     for args, kwargs in calls:
@@ -448,7 +498,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         w_mean = (wsum / rows).float()
         # parent: forward closure over the calibration batches
         if r.parent_kind == "module":
-            calls = _tokenwise_concat(r.parent, caches[r.smooth_name].calls)
+            calls = caches[r.smooth_name].calls
+            calls = _tokenwise_concat(r.parent, calls) if _is_tokenwise(r.parent) else _batchwise_concat(calls)
             run: Callable[[], List[torch.Tensor]] = lambda p=r.parent, c=calls: _run_parent(p, c)
         else:
             ei = experts[id(b0.module)]
