@@ -115,10 +115,41 @@ __device__ __forceinline__ float bf16_div(float d, float c) {
   return bfr(q);
 }
 
+// Code stores are sc1 (write-through): a plain or nt store leaves the line dirty in the XCD's
+// L2, and the end-of-kernel release then writes the launch's last outputs back serially, in the
+// kernel's tail.  Measured on MI355X (scripts/tune_ab.sh, interleaved rounds): int4 g128
+// [11008, 4096] 20.3 -> 19.7 us, MXFP4 21.0 -> 20.7, FP8 g32 22.7 -> 22.5, and in the large-launch
+// (nt-load) path int4 g128 [44032, 4096] 72.7 -> 69.8 us, FP8 g32 84.0 -> 78.6 us (7.0 TB/s).
+// The 2-byte scale stores stay plain: as sc1 each is its own fabric write (no gain measured).
+#ifndef QZ_SC1
+#define QZ_SC1 2  // 0 = plain stores, 1 = sc1 code + scale stores, 2 = sc1 code stores
+#endif
+#ifndef QZ_SC1_NT
+#define QZ_SC1_NT 1  // sc1 instead of nt code stores in the large-launch path
+#endif
+// sc1 store (relaxed agent-scope atomic store = global_store_* sc1)
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, const T v) {
+  if constexpr (sizeof(T) == 2) {
+    __hip_atomic_store(reinterpret_cast<uint16_t*>(p), __builtin_bit_cast(uint16_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 4) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (sizeof(T) == 8) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *p = v;
+  }
+}
+
 // output stores; NTS = non-temporal (streaming outputs of launches far larger than the MALL)
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_out(T* p, const T v) {
-  if constexpr (NTS) {
+  if constexpr (((QZ_SC1 != 0 && !NTS) || (QZ_SC1_NT && NTS)) && sizeof(T) <= 8) {
+    st_sc1(p, v);
+  } else if constexpr (NTS) {
     if constexpr (sizeof(T) == 4) {
       __builtin_nontemporal_store(__builtin_bit_cast(uint32_t, v), reinterpret_cast<uint32_t*>(p));
     } else if constexpr (sizeof(T) == 8) {
@@ -357,8 +388,12 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   encode_store<KIND, FQ, SYM, NTS>(A, ps, g, x, cs, unit);
   if ((lane & (L - 1)) == 0) {
     const int64_t gi = unit >> LOGL;
-    if (A.scale_bytes == 2) reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
-    else reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
+    if (A.scale_bytes == 2) {
+      if constexpr (QZ_SC1 == 1 && !NTS) st_sc1(reinterpret_cast<uint16_t*>(A.s_out) + gi, (uint16_t)g.sbits);
+      else reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
+    } else {
+      reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
+    }
     if (A.zp_out) A.zp_out[gi] = (int8_t)g.zp;
   }
 }
