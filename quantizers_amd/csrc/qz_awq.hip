@@ -300,7 +300,7 @@ __global__ __launch_bounds__(256) void k_scale_v8(uint16_t* w, int64_t R, int64_
       const float y0 = divide ? x0 / s0 : x0 * s0, y1 = divide ? x1 / s1 : x1 * s1;
       o[k] = (uint32_t)f2bf(y0) | ((uint32_t)f2bf(y1) << 16);
     }
-    *p = make_uint4(o[0], o[1], o[2], o[3]);
+    st16_wt(p, make_uint4(o[0], o[1], o[2], o[3]));
   }
 }
 

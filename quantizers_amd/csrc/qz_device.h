@@ -35,6 +35,23 @@ __device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(ui
 // round an f32 result to bf16 (RNE, v_cvt_pk_bf16_f32) and widen back
 __device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
 
+#ifndef QZ_SC1_16
+#define QZ_SC1_16 1  // 16-B output stores write-through (sc1); 0 = plain (tuning knob)
+#endif
+// 16-B write-through (sc1) global store: the line does not stay dirty in the XCD's L2, so the
+// end-of-kernel release has nothing to write back (MI355X_MICROARCH.md: 16-B sc1 store ~ plain).
+// The trailing s_nop keeps the compiler's next instruction off the data VGPRs until the store
+// has read them (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void st16_wt(void* p, const uint4 v) {
+#if QZ_SC1_16
+  typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+#else
+  *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+
 // torch.clamp: NaN propagates
 __device__ __forceinline__ float clamp_t(float x, float lo, float hi) {
   return (x != x) ? x : fminf(fmaxf(x, lo), hi);

@@ -26,6 +26,14 @@ constexpr int BLOCK = 256;
 #define QZ_UNROLL 2
 #endif
 constexpr int UNROLL = QZ_UNROLL;  // 16-B units per lane per tile
+#ifndef QZ_UNROLL_NT
+#define QZ_UNROLL_NT 4
+#endif
+// units per lane in the large-launch (nt) quantize path: 4 KiB tiles keep more bytes in flight
+// per wave; [44032, 4096] int4 g128 72.6 -> 69.3 us (at 90 MB per launch UNROLL 4 loses: 21.0 vs 20.7)
+constexpr int UNROLL_NT = QZ_UNROLL_NT;
+// tile size (units per lane) of a k_group_fast instantiation
+constexpr int tile_unroll(bool fq, bool nt) { return (nt && !fq) ? UNROLL_NT : UNROLL; }
 #ifndef QZ_FAST_BLOCK
 #define QZ_FAST_BLOCK 128
 #endif
@@ -149,6 +157,8 @@ template <bool NTS, typename T>
 __device__ __forceinline__ void st_out(T* p, const T v) {
   if constexpr (((QZ_SC1 != 0 && !NTS) || (QZ_SC1_NT && NTS)) && sizeof(T) <= 8) {
     st_sc1(p, v);
+  } else if constexpr (((QZ_SC1 != 0 && !NTS) || (QZ_SC1_NT && NTS)) && sizeof(T) == 16) {
+    st16_wt(p, __builtin_bit_cast(uint4, v));
   } else if constexpr (NTS) {
     if constexpr (sizeof(T) == 4) {
       __builtin_nontemporal_store(__builtin_bit_cast(uint32_t, v), reinterpret_cast<uint32_t*>(p));
@@ -398,7 +408,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
 }
 
-template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS = false>
+template <int LOGL, int KIND, bool FQ, bool SYM, bool NTS, int UNROLL>
 __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, const uint4* v, int64_t b, int64_t tile,
                                              int lane, const f32x2 (*csu)[4]) {
   const float gs = (KIND == K_NV) ? A.gscale[b] : 0.f;
@@ -429,6 +439,7 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
 // loads branch-free.  grid = (tiles per slice, batch): slices may be strided (fused experts).
 template <int LOGL, int KIND, bool FQ, bool SYM, bool NT = false>
 __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
+  constexpr int UNROLL = tile_unroll(FQ, NT);
   __shared__ uint4 lds_buf[FBLOCK / WAVE][UNROLL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x >> 6;
@@ -480,7 +491,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
 #endif
-  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES>(A, p, v, b, tile, lane, csu);
+  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES, UNROLL>(A, p, v, b, tile, lane, csu);
 }
 
 // --------------------------------------------------------------- single-pass tile path
@@ -1112,9 +1123,9 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.cs_ld_batch = cs_ld_batch;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
-    const int64_t n_tiles = cdiv(F.units_per_batch, UNROLL * WAVE);
-    const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
     const bool nt = batch * rows * cols * 2 > QZ_NT_BYTES;
+    const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(fq, nt) * WAVE);
+    const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
                        dim3(FBLOCK), 0, st, F);
     return launch_err();

@@ -27,9 +27,62 @@ def load(path):
     return lib
 
 
+def awq_main(paths, libs):
+    """MODE=awq: the AWQ fake-quant Q(W*s)/s (int4 g128) and the in-place column smoothing."""
+    dev = torch.device("cuda:0")
+    ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
+    s = (torch.rand(COLS, device=dev) + 0.5).float()
+    out = torch.empty_like(ws[0])
+    a = _lib.QzArgs(4, 0, 1, 2, G, 0, 0, 0)
+    for lib in libs:
+        lib.qz_awq_fake_quant.argtypes = [P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.POINTER(_lib.QzArgs), P, P, P, ctypes.c_size_t, P]
+        lib.qz_scale_columns.argtypes = [P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, P, ctypes.c_int32, P]
+    n = libs[0].qz_quantize_workspace_size(1, ROWS, COLS, ctypes.byref(a))
+    wsp = torch.empty(n + 256, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream()
+    sp = P(st.cuda_stream)
+    ops = {
+        "fake_quant": (lambda lib, i: lib.qz_awq_fake_quant(P(ws[i % COPIES].data_ptr()), 1, ROWS, COLS, COLS,
+                                                            ROWS * COLS, ctypes.byref(a), P(s.data_ptr()),
+                                                            P(out.data_ptr()), P(wsp.data_ptr()), wsp.numel(), sp),
+                       ROWS * COLS * 4),
+        "scale_columns": (lambda lib, i: lib.qz_scale_columns(P(ws[i % COPIES].data_ptr()), ROWS, COLS, COLS,
+                                                              P(s.data_ptr()), i & 1, sp), ROWS * COLS * 4),
+    }
+    ref = None
+    for lib in libs:
+        assert ops["fake_quant"][0](lib, 0) == 0
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        elif not torch.equal(ref.view(torch.int16), out.view(torch.int16)):
+            print(f"NOTE: {lib._name} fake-quant output differs")
+    K = int(os.environ.get("K", 60))
+    for name, (fn, nbytes) in ops.items():
+        res = {p: [] for p in paths}
+        for rnd in range(int(os.environ.get("ROUNDS", 8))):
+            for p, lib in zip(paths, libs):
+                for i in range(10):
+                    fn(lib, i)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for i in range(K):
+                    fn(lib, i)
+                e1.record(st)
+                torch.cuda.synchronize()
+                res[p].append(e0.elapsed_time(e1) * 1e3 / K)
+        for p in paths:
+            v = sorted(res[p])
+            print(f"{name:14s} {os.path.basename(p):22s} median {v[len(v)//2]:7.2f} us  min {v[0]:7.2f} us  "
+                  f"-> {nbytes / (v[len(v)//2] * 1e-6) / 1e9:7.0f} GB/s alg")
+
+
 def main():
     paths = sys.argv[1:]
     libs = [load(p) for p in paths]
+    if os.environ.get("MODE") == "awq":
+        return awq_main(paths, libs)
     dev = torch.device("cuda:0")
     ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
     if KIND == "int":
