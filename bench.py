@@ -3,10 +3,13 @@
 bf16 weight [11008, 4096] (BASELINE.json configs[1]: "Qwen3-4B AWQ int4 group_size=128 on
 1xMI355X"; metric "params quantized/sec + achieved HBM GB/s").
 
-One *step* = one fused quantize+pack pass (qz_quantize, one kernel launch) over one
-[11008, 4096] bf16 weight already resident in HBM.  The step rotates over COPIES distinct
-input buffers (> the 256 MiB Infinity Cache) so every step streams its weight from HBM, not L3
-(BASELINE.md timing protocol).  Multi-GPU: one process per GPU, each quantizes its own weight
+One *step* = one fused quantize+pack pass over one [11008, 4096] bf16 weight already resident
+in HBM, into that step's own output tensors.  The step rotates over COPIES distinct input buffers
+(> the 256 MiB Infinity Cache) so every step streams its weight from HBM, not L3 (BASELINE.md
+timing protocol).  The K timed steps are ONE grouped launch (qz_quantize_grouped: grid.y = step,
+a device table of per-step weight/output pointers), the way the library quantizes many
+same-shape weights; the one-launch-per-weight rate (qz_quantize_many) is reported beside it
+(``per_weight_launch``), and ``--per-weight-launch`` makes it the timed path.  Multi-GPU: one process per GPU, each quantizes its own weight
 shard set (weak scaling, no collective in the timed region); after timing, ranks reassemble
 the packed tensors with one RCCL all-gather (reported separately, as the north star asks).
 
@@ -33,7 +36,13 @@ PARAMS = ROWS * COLS
 ALG_BYTES = PARAMS * 2 + PARAMS * BITS // 8 + (PARAMS // GROUP) * 2  # 113,426,432
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128"
-KERNEL_NAME = "k_group_fast<4, 0, false, true, false>"
+KERNEL_NAME_SINGLE = "k_group_fast<4, 0, false, true, false>"  # one launch per weight (90 MB < 256 MiB)
+NT_BYTES = 256 << 20  # QZ_NT_BYTES: launches reading more use nt loads + 4 KiB tiles
+
+
+def grouped_kernel_name(k):
+    nt = k * PARAMS * 2 > NT_BYTES
+    return f"k_group_fast<4, 0, false, true, {str(nt).lower()}, true>"
 
 # Qwen3-4B linear shapes (hidden 2560, inter 9728, 32 q / 8 kv heads x 128), 36 layers
 QWEN3_4B = [("q_proj", 4096, 2560), ("k_proj", 1024, 2560), ("v_proj", 1024, 2560), ("o_proj", 2560, 4096),
@@ -50,6 +59,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-model-pass", action="store_true")
+    p.add_argument("--per-weight-launch", action="store_true",
+                   help="time one qz_quantize launch per step (qz_quantize_many) instead of one grouped launch")
     p.add_argument("--python-loop", action="store_true",
                    help="one Python qz_quantize call per step instead of one qz_quantize_many call")
     p.add_argument("--graph", action="store_true",
@@ -73,16 +84,18 @@ def cpu_model():
 def cpu_baseline(seconds: float, measured=None):
     """The oracle's torch-op restatement of compressed-tensors (oracle/ct_torch.py), timed on the
     host cores on the same synthetic weight.  The oracle is used only here (the
-    CPU leg): besides the timing it checks the GPU's measured output slice ``measured`` =
-    (input rows, packed codes, scales) bit for bit against the plain-C restatement."""
+    CPU leg): besides the timing it checks the GPU's measured output slices ``measured`` =
+    (input rows, packed codes, scales[, codes, scales of the per-weight launch]) bit for bit
+    against the plain-C restatement."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ct_torch as ct  # CPU baseline leg only
     import qref  # checker only
     ok = None
     if measured is not None:
-        w_in, codes, scale = measured
+        w_in, outs = measured[0], measured[1:]
         ref_p, ref_s = qref.int_sym_group_pack(w_in, BITS, GROUP)
-        ok = bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
+        ok = all(bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
+                 for codes, scale in zip(outs[0::2], outs[1::2]))
 
     threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
     torch.set_num_threads(threads)
@@ -291,13 +304,16 @@ def awq_oneshot_layers(dev, n_layers=2, n_seq=16, seq=2048):
             "projected_36_layers_s": t / n_layers * 36, "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
 
 
-def read_pmc_traffic():
-    """HBM bytes per launch from the committed rocprofv3 PMC passes (profiles/*pmc*.json), or None."""
+def read_pmc_traffic(kernel, weights_per_launch):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json: bytes per weight x the weights one launch processes), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d.get("source")
+        if not d.get("kernel", "").startswith(kernel):
+            return None, None
+        return d["hbm_bytes_per_weight"] * weights_per_launch, d.get("source")
     except Exception:
         return None, None
 
@@ -337,6 +353,22 @@ def main():
     def step(i, st=stream):
         prep.run(copies[i % args.copies], st)
 
+    # Default: the K steps are ONE grouped launch (qz_quantize_grouped) over K (weight, outputs)
+    # pairs: step i reads copy i % COPIES and writes its own codes/scales (K distinct output
+    # sets, so no two steps of the launch write the same bytes).
+    grouped = not (args.per_weight_launch or args.python_loop or args.graph)
+    if grouped:
+        def outs_for(n):
+            return [{"codes": torch.empty_like(bufs["codes"]), "scale": torch.empty_like(bufs["scale"]),
+                     "zero_point": None} for _ in range(n)]
+        # (--profile-only: the warmup launch has the timed launch's size, so every launch of the
+        # grouped kernel in a rocprofv3 pass covers K weights)
+        nw = args.steps if args.profile_only else max(args.warmup, 1)
+        warm = ops.GroupedQuantize([copies[i % args.copies] for i in range(nw)], a, outs=outs_for(nw))
+        gq = ops.GroupedQuantize([copies[i % args.copies] for i in range(args.steps)], a,
+                                 outs=outs_for(args.steps))
+        warm.run(stream)  # W warmup steps (one grouped launch)
+        del warm
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -356,14 +388,16 @@ def main():
         graph.replay()  # untimed: first replay uploads the graph
         torch.cuda.synchronize()
 
-    # Default: the K steps go through qz_quantize_many -- one host call that enqueues the K
-    # qz_quantize launches (one per step, each over its own resident copy) -- so the ~20 us
-    # Python/ctypes cost per call cannot leave the GPU idle between the ~21 us kernels.
+    # One launch per weight: qz_quantize_many -- one host call that enqueues the K qz_quantize
+    # launches (each over its own resident copy, shared outputs) -- so the ~20 us Python/ctypes
+    # cost per call cannot leave the GPU idle between the ~21 us kernels.
     many = None if (graph is not None or args.python_loop) else \
         prep.prepare_many([copies[i % args.copies] for i in range(args.steps)])
 
-    def run_steps():
-        if graph is not None:
+    def run_steps(grouped_launch=grouped):
+        if grouped_launch:
+            gq.run(stream)
+        elif graph is not None:
             graph.replay()
         elif many is not None:
             many(stream)
@@ -376,28 +410,46 @@ def main():
         torch.cuda.synchronize()
         return
 
-    # ---- contract timing: barrier + sync, exactly K steps, sync + barrier, max over ranks.
-    # HIP events on the launch stream bracket the same region: their elapsed time / K is the
-    # kernel's average launch duration (back-to-back launches, no host gaps) for the roofline.
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    run_steps()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    k_ms_mean = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([el], device=dev, dtype=torch.float64)
-    if world > 1:
-        _all_reduce_max(t)
-    el = t.item()
+    def timed_region(grouped_launch):
+        """barrier + sync, exactly K steps, sync + barrier; wall seconds (max over ranks) and the
+        HIP-event time of the region on the launch stream (ms)."""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        run_steps(grouped_launch)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        wall = time.perf_counter() - t0
+        t = torch.tensor([wall], device=dev, dtype=torch.float64)
+        if world > 1:
+            _all_reduce_max(t)
+        return t.item(), ev0.elapsed_time(ev1)
 
-    # ---- secondary: one event pair around each launch (adds the event packets' ~2 us per launch)
+    # ---- contract timing.  HIP events on the launch stream bracket the same region: for the
+    # grouped launch their elapsed time IS the kernel's launch duration; for per-weight launches
+    # elapsed / K is the average launch duration (back-to-back, no host gaps).
+    el, region_ms = timed_region(grouped)
+    n_launches = 1 if grouped else args.steps
+    k_ms_mean = region_ms / n_launches
+
+    # ---- secondary: one launch per weight (qz_quantize_many), same K steps, and one event pair
+    # around each launch (adds the event packets' ~1-2 us per launch)
+    per_weight = None
+    if grouped:  # the same K steps into the same K distinct output sets, one launch per step
+        many = prep.prepare_many([copies[i % args.copies] for i in range(args.steps)], outs=gq.outs)
+        pw_el, pw_region_ms = timed_region(False)
+        pw_us = pw_region_ms / args.steps * 1e3
+        per_weight = {"kernel": KERNEL_NAME_SINGLE, "us_per_launch": pw_us,
+                      "params_per_s": world * PARAMS * args.steps / pw_el,
+                      "achieved_GBps": ALG_BYTES / (pw_us * 1e-6) / 1e9,
+                      "frac": ALG_BYTES / (pw_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                      "timing": "HIP events around K back-to-back qz_quantize launches (one qz_quantize_many call, "
+                                "the K distinct output sets of the grouped launch) / K"}
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     for i in range(args.steps):
@@ -406,6 +458,9 @@ def main():
         ends[i].record(stream)
     torch.cuda.synchronize()
     durs = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
+    if per_weight is not None:
+        per_weight["us_per_launch_events_mean"] = sum(durs) / len(durs) * 1e3
+        per_weight["us_per_launch_events_median"] = durs[len(durs) // 2] * 1e3
     k_ms_each_mean = sum(durs) / len(durs)
     k_ms_each_med = durs[len(durs) // 2]
 
@@ -413,7 +468,13 @@ def main():
     measured = None
     if rank == 0:
         last = (args.steps - 1) % args.copies
-        measured = (copies[last][:256].cpu(), bufs["codes"][:256].cpu(), bufs["scale"][:256].cpu())
+        o_last = gq.outs[args.steps - 1] if grouped else bufs
+        measured = (copies[last][:256].cpu(), o_last["codes"][:256].cpu(), o_last["scale"][:256].cpu())
+        if grouped:  # the per-step event-pair launches wrote bufs from the same copy: must agree too
+            measured = measured + (bufs["codes"][:256].cpu(), bufs["scale"][:256].cpu())
+    if grouped:
+        del gq
+        torch.cuda.empty_cache()
 
     # ---- reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
     allgather = None
@@ -477,8 +538,10 @@ def main():
     if rank == 0:
         ms_step = el / args.steps * 1e3
         value = world * PARAMS * args.steps / el
-        achieved = ALG_BYTES / (k_ms_mean * 1e-3) / 1e9
-        traffic, tsrc = read_pmc_traffic()
+        per_launch = args.steps if grouped else 1  # weights one launch processes
+        kernel = grouped_kernel_name(args.steps) if grouped else KERNEL_NAME_SINGLE
+        achieved = ALG_BYTES * per_launch / (k_ms_mean * 1e-3) / 1e9
+        traffic, tsrc = read_pmc_traffic(kernel, per_launch)
         line = {
             "metric": METRIC,
             "value": value,
@@ -499,14 +562,18 @@ def main():
             "hbm_GBps_step": world * ALG_BYTES * args.steps / el / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": KERNEL_NAME, "kernel_ms_mean": k_ms_mean,
-                         "kernel_timing": "HIP events around the K back-to-back launches of the timed region / K"
-                                          + (" (one hipGraph replay)" if graph is not None else
-                                             " (one qz_quantize_many call)" if many is not None else
-                                             " (Python loop of qz_quantize calls)"),
-                         "kernel_ms_per_launch_events_mean": k_ms_each_mean,
-                         "kernel_ms_per_launch_events_median": k_ms_each_med,
-                         "alg_bytes_per_launch": ALG_BYTES, "traffic_source": tsrc},
+                         "kernel": kernel, "kernel_ms_mean": k_ms_mean, "weights_per_launch": per_launch,
+                         "kernel_timing": ("HIP events around the timed region = the one grouped launch "
+                                           "(qz_quantize_grouped) of the K steps" if grouped else
+                                           "HIP events around the K back-to-back launches of the timed region / K"
+                                           + (" (one hipGraph replay)" if graph is not None else
+                                              " (one qz_quantize_many call)" if many is not None else
+                                              " (Python loop of qz_quantize calls)")),
+                         "alg_bytes_per_launch": ALG_BYTES * per_launch,
+                         "alg_bytes_per_weight": ALG_BYTES, "traffic_source": tsrc},
+            "per_weight_launch": per_weight if grouped else {
+                "kernel": KERNEL_NAME_SINGLE, "us_per_launch_events_mean": k_ms_each_mean * 1e3,
+                "us_per_launch_events_median": k_ms_each_med * 1e3},
             "cpu_baseline": cpu,
             "parity_check": ok,
             "allgather_ms": allgather,

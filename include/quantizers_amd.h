@@ -117,6 +117,22 @@ int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* 
                      int32_t out_fmt, void* workspace, size_t workspace_bytes, qz_stream_t stream);
 
 /*
+ * qz_quantize_grouped -- qz_quantize over n independent dense [rows, cols] weights of one shape
+ * and one scheme in ONE launch (grid.y = weight), like a grouped GEMM: the per-launch ramp-up and
+ * drain (~3 us on MI355X) is paid once for the group instead of once per weight.  Replaces the
+ * same per-module compressor loop as qz_quantize_many (do_oneshot.py:197).  `table` is a DEVICE
+ * array of 4*n uint64 written by the caller before the launch (stream order):
+ *   table[i] = weight i (bf16, dense, 16-B aligned), table[n+i] = its codes, table[2n+i] = its
+ *   scales, table[3n+i] = its int8 zero points (required for asymmetric schemes, else 0).
+ * Output layouts are exactly qz_quantize's with batch = 1.  No weight may alias any output.
+ * Single-pass group schemes only (GROUP / TENSOR_GROUP with a power-of-two group 8..512, int /
+ * FP8 / MXFP4 / FP4, not NVFP4 and not fake-quant): anything else returns QZ_ERR_FORMAT and the
+ * caller uses qz_quantize_many.  n <= 65535.  No workspace.
+ */
+int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t cols,
+                        const qz_args* a, int32_t out_fmt, qz_stream_t stream);
+
+/*
  * qz_quantize_qparams -- quantize with caller-supplied qparams (stateful observers such as the
  * recipes' `minmax`, recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:48).  Replaces [3P]
  * compressed-tensors quantize(x, scale, zero_point, args) / fake_quantize(...).

@@ -28,7 +28,7 @@ EXPORTS = (
     "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_accum",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
-    "qz_awq_sq_err_accum", "qz_quantize_many",
+    "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped",
 )
 
 
@@ -62,6 +62,7 @@ def load() -> ctypes.CDLL:
         "qz_quantize_workspace_size": ([I64, I64, I64, A], SZ),
         "qz_quantize": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P, SZ, P], ctypes.c_int),
         "qz_quantize_many": ([I64, P, P, P, P, P, I64, I64, I64, I64, I64, A, I32, P, SZ, P], ctypes.c_int),
+        "qz_quantize_grouped": ([I64, P, I64, I64, A, I32, P], ctypes.c_int),
         "qz_quantize_qparams": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P], ctypes.c_int),
         "qz_observe_minmax": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
         "qz_calculate_qparams": ([P, P, I64, A, P, P, P, P], ctypes.c_int),

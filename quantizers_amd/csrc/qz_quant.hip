@@ -27,10 +27,11 @@ constexpr int BLOCK = 256;
 #endif
 constexpr int UNROLL = QZ_UNROLL;  // 16-B units per lane per tile
 #ifndef QZ_UNROLL_NT
-#define QZ_UNROLL_NT 4
+#define QZ_UNROLL_NT 2
 #endif
-// units per lane in the large-launch (nt) quantize path: 4 KiB tiles keep more bytes in flight
-// per wave; [44032, 4096] int4 g128 72.6 -> 69.3 us (at 90 MB per launch UNROLL 4 loses: 21.0 vs 20.7)
+// units per lane in the nt quantize path (tuning knob): 4 KiB tiles won (72.6 -> 69.3 us at
+// [44032, 4096]) only while the outputs stayed MALL-resident; with distinct outputs per weight
+// UNROLL 2 / 3 / 4 run 17.8 / 19.5 / 20.1 us per weight (grouped launches)
 constexpr int UNROLL_NT = QZ_UNROLL_NT;
 // tile size (units per lane) of a k_group_fast instantiation
 constexpr int tile_unroll(bool fq, bool nt) { return (nt && !fq) ? UNROLL_NT : UNROLL; }
@@ -75,6 +76,10 @@ struct FastArgs {
   const float* gscale;      // [batch], NVFP4
   const float* col_scales;  // [cols] (+ b * cs_ld_batch), AWQ prescale (FQ only)
   int64_t cs_ld_batch;      // 0: one scale vector for every slice; cols: one per slice
+  // grouped launch (qz_quantize_grouped): device table [4][n_tab] of per-weight pointers
+  // {weight, codes, scale, zero point or 0}; blockIdx.y selects the weight
+  const uint64_t* tab;
+  int64_t n_tab;
 };
 
 // --------------------------------------------------------------- single-pass path
@@ -88,7 +93,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define QZ_HW_FP4 1
 #endif
 #ifndef QZ_NT_BYTES
-#define QZ_NT_BYTES (256ll << 20)  // weight bytes per launch above which loads are non-temporal
+#define QZ_NT_BYTES (256ll << 20)  // fake-quant: weight bytes per launch above which loads are non-temporal
+#endif
+// quantize (+pack): weight bytes per launch above which the group path streams non-temporally
+// (nt loads + nt stores).  Measured with DISTINCT output tensors per weight, as a whole-model pass
+// writes them (scripts/tune_fast.py OUTS=48 / MODE=grouped): the read-once weight must not take
+// the MALL from the outputs, at every size -- int4 g128 [11008, 4096] per launch 21.4 -> 20.8 us,
+// FP8 g32 25.3 -> 23.2 us, grouped launches 17.8 -> 17.3 us per weight (the sc1 stores measured
+// better only while one shared output buffer stayed MALL-resident).
+#ifndef QZ_NT_BYTES_Q
+#define QZ_NT_BYTES_Q 0
 #endif
 #ifndef QZ_NT_STORES
 #define QZ_NT_STORES 1  // non-temporal output stores in the NT (large-launch) group path
@@ -97,7 +111,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define QZ_TILE_NT 1  // non-temporal register loads in the tile path above QZ_NT_BYTES
 #endif
 #ifndef QZ_REG_LOADS
-#define QZ_REG_LOADS 0
+#define QZ_REG_LOADS 0  // per-weight launches: LDS-DMA staging (23.1 -> 21.5 us vs register loads)
+#endif
+#ifndef QZ_REG_LOADS_GRP
+#define QZ_REG_LOADS_GRP 1  // grouped launches: register loads (17.95 -> 17.51 us per weight)
 #endif
 #ifndef QZ_LDS_AUX
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
@@ -123,17 +140,17 @@ __device__ __forceinline__ float bf16_div(float d, float c) {
   return bfr(q);
 }
 
-// Code stores are sc1 (write-through): a plain or nt store leaves the line dirty in the XCD's
-// L2, and the end-of-kernel release then writes the launch's last outputs back serially, in the
-// kernel's tail.  Measured on MI355X (scripts/tune_ab.sh, interleaved rounds): int4 g128
-// [11008, 4096] 20.3 -> 19.7 us, MXFP4 21.0 -> 20.7, FP8 g32 22.7 -> 22.5, and in the large-launch
-// (nt-load) path int4 g128 [44032, 4096] 72.7 -> 69.8 us, FP8 g32 84.0 -> 78.6 us (7.0 TB/s).
-// The 2-byte scale stores stay plain: as sc1 each is its own fabric write (no gain measured).
+// Output stores outside the nt quantize path (the tile path, fake-quant, smoothing) are sc1
+// (write-through): a plain store leaves the line dirty in the XCD's L2 and the end-of-kernel
+// release writes it back in the kernel's tail (fake-quant [11008, 4096] 39.6 -> 37.3 us, smoothing
+// 33.7 -> 31.1 us, FP8_BLOCK 25.4 -> 23.6 us; scripts/tune_ab.sh).  In the nt quantize path nt
+// stores win once the outputs are distinct per weight (QZ_NT_BYTES_Q).  The 2-byte scale stores
+// stay plain: as sc1 each is its own fabric write (no gain measured).
 #ifndef QZ_SC1
 #define QZ_SC1 2  // 0 = plain stores, 1 = sc1 code + scale stores, 2 = sc1 code stores
 #endif
 #ifndef QZ_SC1_NT
-#define QZ_SC1_NT 1  // sc1 instead of nt code stores in the large-launch path
+#define QZ_SC1_NT 0  // sc1 instead of nt code stores in the nt path (tuning knob)
 #endif
 // sc1 store (relaxed agent-scope atomic store = global_store_* sc1)
 template <typename T>
@@ -437,36 +454,46 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
 // persistent grid-stride loop with register double-buffering is slower than one-shot waves.
 // Out-of-range lanes re-load the slice's last unit (results never stored), keeping the
 // loads branch-free.  grid = (tiles per slice, batch): slices may be strided (fused experts).
-template <int LOGL, int KIND, bool FQ, bool SYM, bool NT = false>
-__global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
+template <int LOGL, int KIND, bool FQ, bool SYM, bool NT = false, bool GRP = false>
+__global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
   constexpr int UNROLL = tile_unroll(FQ, NT);
   __shared__ uint4 lds_buf[FBLOCK / WAVE][UNROLL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x >> 6;
   const int64_t tile = (int64_t)blockIdx.x * (FBLOCK / WAVE) + w;
-  const int64_t tiles = (A.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
+  const int64_t tiles = (A0.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
   if (tile >= tiles) return;
-  const int64_t b = blockIdx.y;
+  FastArgs A = A0;
+  int64_t b = blockIdx.y;
+  if constexpr (GRP) {  // grouped launch: this workgroup's weight and outputs from the table
+    A.w = reinterpret_cast<const uint16_t*>(A0.tab[b]);
+    A.q_out = reinterpret_cast<void*>(A0.tab[A0.n_tab + b]);
+    A.s_out = reinterpret_cast<void*>(A0.tab[2 * A0.n_tab + b]);
+    A.zp_out = reinterpret_cast<int8_t*>(A0.tab[3 * A0.n_tab + b]);
+    b = 0;
+  }
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
-#if QZ_REG_LOADS  // tuning knob: direct-to-register 16-B loads instead of the LDS-DMA staging
+  // direct-to-register 16-B loads (grouped launches) or LDS-DMA staging (per-weight launches)
+  constexpr bool REG = GRP ? QZ_REG_LOADS_GRP : QZ_REG_LOADS;
   uint4 v[UNROLL];
+  if constexpr (REG) {
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
-    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
-    if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + unit)));
-    else v[u] = src[unit];
-  }
-#else
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+      unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
+      if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + unit)));
+      else v[u] = src[unit];
+    }
+  } else {
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) {
-    int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
-    unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
-    __builtin_amdgcn_global_load_lds((const void*)(src + unit),
-                                     (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
-                                     NT ? 2 : QZ_LDS_AUX);
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t unit = tile * (UNROLL * WAVE) + u * WAVE + lane;
+      unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(src + unit),
+                                       (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
+                                       NT ? 2 : QZ_LDS_AUX);
+    }
   }
-#endif
   // AWQ fake-quant: fetch this lane's column scales while the DMA is in flight
   f32x2 csu[UNROLL][4];
   if (FQ && A.col_scales) {
@@ -485,12 +512,11 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A) {
   }
   QP p = A.p;
   p.kind = KIND;
-#if !QZ_REG_LOADS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
-  uint4 v[UNROLL];
+  if constexpr (!REG) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA has landed in LDS
 #pragma unroll
-  for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
-#endif
+    for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
+  }
   process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES, UNROLL>(A, p, v, b, tile, lane, csu);
 }
 
@@ -835,30 +861,35 @@ using FastFn = void (*)(FastArgs);
 
 // fq: AWQ fake-quant; nt: non-temporal weight stream (launches much larger than the 256 MiB
 // Infinity Cache: the read-once weight should not evict the outputs; +6 % at 360 MB, -2 % at 90 MB)
+// grp: grouped launch over a device pointer table (quantize only; NVFP4 needs its per-tensor pass)
 template <int LOGL, int KIND, bool SYM>
-FastFn pick_fq(bool fq, bool nt) {
+FastFn pick_fq(bool fq, bool nt, bool grp) {
+  if constexpr (KIND != K_NV) {
+    if (grp) return nt ? (FastFn)k_group_fast<LOGL, KIND, false, SYM, true, true>
+                       : (FastFn)k_group_fast<LOGL, KIND, false, SYM, false, true>;
+  }
   if (fq) return nt ? (FastFn)k_group_fast<LOGL, KIND, true, SYM, true> : (FastFn)k_group_fast<LOGL, KIND, true, SYM>;
   return nt ? (FastFn)k_group_fast<LOGL, KIND, false, SYM, true> : (FastFn)k_group_fast<LOGL, KIND, false, SYM>;
 }
 template <int LOGL>
-FastFn pick_kind(int kind, bool sym, bool fq, bool nt) {
+FastFn pick_kind(int kind, bool sym, bool fq, bool nt, bool grp) {
   switch (kind) {
-    case K_INT: return sym ? pick_fq<LOGL, K_INT, true>(fq, nt) : pick_fq<LOGL, K_INT, false>(fq, nt);
-    case K_FP8: return pick_fq<LOGL, K_FP8, true>(fq, nt);
-    case K_MX: return pick_fq<LOGL, K_MX, true>(fq, nt);
-    case K_NV: return pick_fq<LOGL, K_NV, true>(fq, nt);
-    default: return pick_fq<LOGL, K_FP4, true>(fq, nt);
+    case K_INT: return sym ? pick_fq<LOGL, K_INT, true>(fq, nt, grp) : pick_fq<LOGL, K_INT, false>(fq, nt, grp);
+    case K_FP8: return pick_fq<LOGL, K_FP8, true>(fq, nt, grp);
+    case K_MX: return pick_fq<LOGL, K_MX, true>(fq, nt, grp);
+    case K_NV: return pick_fq<LOGL, K_NV, true>(fq, nt, grp);
+    default: return pick_fq<LOGL, K_FP4, true>(fq, nt, grp);
   }
 }
-FastFn pick_fast(int logl, int kind, bool sym, bool fq, bool nt) {
+FastFn pick_fast(int logl, int kind, bool sym, bool fq, bool nt, bool grp = false) {
   switch (logl) {
-    case 0: return pick_kind<0>(kind, sym, fq, nt);
-    case 1: return pick_kind<1>(kind, sym, fq, nt);
-    case 2: return pick_kind<2>(kind, sym, fq, nt);
-    case 3: return pick_kind<3>(kind, sym, fq, nt);
-    case 4: return pick_kind<4>(kind, sym, fq, nt);
-    case 5: return pick_kind<5>(kind, sym, fq, nt);
-    default: return pick_kind<6>(kind, sym, fq, nt);
+    case 0: return pick_kind<0>(kind, sym, fq, nt, grp);
+    case 1: return pick_kind<1>(kind, sym, fq, nt, grp);
+    case 2: return pick_kind<2>(kind, sym, fq, nt, grp);
+    case 3: return pick_kind<3>(kind, sym, fq, nt, grp);
+    case 4: return pick_kind<4>(kind, sym, fq, nt, grp);
+    case 5: return pick_kind<5>(kind, sym, fq, nt, grp);
+    default: return pick_kind<6>(kind, sym, fq, nt, grp);
   }
 }
 
@@ -1121,9 +1152,11 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.gscale = gs_dst;
     F.col_scales = col_scales;
     F.cs_ld_batch = cs_ld_batch;
+    F.tab = nullptr;
+    F.n_tab = 0;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
-    const bool nt = batch * rows * cols * 2 > QZ_NT_BYTES;
+    const bool nt = batch * rows * cols * 2 > (fq ? QZ_NT_BYTES : QZ_NT_BYTES_Q);
     const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(fq, nt) * WAVE);
     const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
@@ -1157,6 +1190,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       F.gscale = gs_dst;
       F.col_scales = nullptr;
       F.cs_ld_batch = 0;
+      F.tab = nullptr;
+      F.n_tab = 0;
       TileArgs T;
       T.rows = rows;
       T.tile_rows = th;
@@ -1209,6 +1244,48 @@ int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* 
     if (rc) return rc;
   }
   return QZ_OK;
+}
+
+int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t cols, const qz_args* a,
+                        int32_t out_fmt, qz_stream_t stream) {
+  if (n == 0) return QZ_OK;
+  if (n < 0 || n > 65535 || rows <= 0 || cols <= 0) return QZ_ERR_SHAPE;
+  if (!table || !a) return QZ_ERR_NULL;
+  Plan pl;
+  int rc = make_plan(a, rows, cols, &pl);
+  if (rc) return rc;
+  if ((rc = check_out_fmt(pl, out_fmt))) return rc;
+  const int64_t g = a->group_size;
+  const bool grp = a->strategy == QZ_GROUP || a->strategy == QZ_TENSOR_GROUP;
+  const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
+  const bool pack_ok = !(pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits != 4 && a->num_bits != 8);
+  // the single-pass group path only (no per-tensor pre-pass, no fake-quant)
+  if (!grp || !pow2 || !pack_ok || pl.kind == K_NV || out_fmt == QZ_OUT_FAKEQUANT || cols % 8) return QZ_ERR_FORMAT;
+  if (!aligned(table, 8)) return QZ_ERR_ALIGN;
+  FastArgs F;
+  F.w = nullptr;
+  F.n_units = rows * cols / 8;
+  F.units_per_batch = rows * cols / 8;
+  F.units_per_row = cols / 8;
+  F.ld_batch = rows * cols;
+  F.p = pl.p;
+  F.out_fmt = out_fmt;
+  F.scale_bytes = pl.scale_bytes;
+  F.q_out = F.s_out = nullptr;
+  F.zp_out = nullptr;
+  F.gscale = nullptr;
+  F.col_scales = nullptr;
+  F.cs_ld_batch = 0;
+  F.tab = table;
+  F.n_tab = n;
+  int logl = 0;
+  while ((8 << logl) < g) ++logl;
+  const bool nt = n * rows * cols * 2 > QZ_NT_BYTES_Q;
+  const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(false, nt) * WAVE);
+  const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
+  hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, nt, true), dim3((unsigned)blocks, (unsigned)n),
+                     dim3(FBLOCK), 0, (hipStream_t)stream, F);
+  return launch_err();
 }
 
 int qz_awq_fake_quant(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,

@@ -23,7 +23,7 @@ slices ``[E, N, K]`` (fused MoE experts).  There is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
-from typing import Callable, Dict, Optional, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -159,6 +159,93 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
     _lib.check(rc, "qz_quantize")
     o.pop("workspace", None)
     return o
+
+
+def grouped_ok(a: QuantizationArgs, w: torch.Tensor) -> bool:
+    """True when qz_quantize_grouped covers this scheme and weight (the single-pass group path)."""
+    g = a.group_size or 0
+    return (a.strategy in ("group", "tensor_group") and not a.is_nvfp4 and 8 <= g <= 512 and (g & (g - 1)) == 0
+            and w.dim() == 2 and w.is_contiguous() and w.dtype == torch.bfloat16 and w.shape[1] % g == 0
+            and w.data_ptr() % 16 == 0)
+
+
+class GroupedQuantize:
+    """``qz_quantize_grouped``: n same-shape dense weights quantized in ONE launch (grid.y =
+    weight), the per-launch ramp paid once.  The device pointer table is built once here;
+    ``run(stream=None)`` is one ctypes call + one kernel launch.  Outputs are exactly
+    ``quantize_weight``'s, one dict per weight (``outs``; allocated when not given)."""
+
+    def __init__(self, ws: Sequence[torch.Tensor], a: QuantizationArgs, out_fmt: Optional[int] = None,
+                 outs: Optional[Sequence[Dict[str, torch.Tensor]]] = None):
+        if not ws:
+            raise ValueError("GroupedQuantize needs at least one weight")
+        if len(ws) > 65535:
+            raise ValueError("GroupedQuantize: at most 65535 weights per launch")
+        shape = tuple(ws[0].shape)
+        for w in ws:
+            _check_dev(w, "weight")
+            if tuple(w.shape) != shape or not grouped_ok(a, w) or w.device != ws[0].device:
+                raise ValueError("GroupedQuantize: every weight must be a dense, 16-B aligned bf16 [rows, cols] "
+                                 "tensor of one shape on one device, under a single-pass group scheme")
+        r, c = shape
+        dev = ws[0].device
+        self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+        self.ca = a.to_c()
+        gshape = n_groups(a, r, c)
+        if outs is None:
+            outs = [{"codes": _alloc_codes(self.out_fmt, a, (), r, c, dev),
+                     "scale": torch.empty(*gshape, dtype=_scale_dtype(a), device=dev),
+                     "zero_point": None if a.symmetric else torch.empty(*gshape, dtype=torch.int8, device=dev)}
+                    for _ in ws]
+        if len(outs) != len(ws):
+            raise ValueError("GroupedQuantize: one output dict per weight")
+        in_ranges = [(w.data_ptr(), w.data_ptr() + w.numel() * 2) for w in ws]
+        for o in outs:
+            for k in ("codes", "scale", "zero_point"):
+                t = o.get(k)
+                if t is None:
+                    continue
+                lo, hi = t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()
+                if any(lo < b_ and a_ < hi for a_, b_ in in_ranges):
+                    raise ValueError("GroupedQuantize: an output aliases a weight")
+        if not a.symmetric and any(o.get("zero_point") is None for o in outs):
+            raise ValueError("GroupedQuantize: asymmetric schemes need a zero_point output per weight")
+        n = len(ws)
+        rows = [[w.data_ptr() for w in ws], [o["codes"].data_ptr() for o in outs],
+                [o["scale"].data_ptr() for o in outs],
+                [0 if o.get("zero_point") is None else o["zero_point"].data_ptr() for o in outs]]
+        self.table = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev)
+        self.n, self.rows, self.cols = n, r, c
+        self.weights, self.outs = list(ws), list(outs)  # keep every pointer alive
+        self.lib = _lib.load()
+
+    def run(self, stream=None) -> List[Dict[str, torch.Tensor]]:
+        st = _P(stream.cuda_stream) if stream is not None else _stream()
+        rc = self.lib.qz_quantize_grouped(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
+                                          self.out_fmt, st)
+        _lib.check(rc, "qz_quantize_grouped")
+        return self.outs
+
+
+def quantize_weights(ws: Sequence[torch.Tensor], a: QuantizationArgs,
+                     out_fmt: Optional[int] = None) -> List[Dict[str, torch.Tensor]]:
+    """Quantize many weights of one scheme: same-shape dense weights under a single-pass group
+    scheme go through ONE grouped launch per shape (qz_quantize_grouped); anything else is one
+    ``quantize_weight`` launch per weight.  Results are identical either way."""
+    res: List[Optional[Dict[str, torch.Tensor]]] = [None] * len(ws)
+    by_shape: Dict[tuple, List[int]] = {}
+    for i, w in enumerate(ws):
+        if grouped_ok(a, w):
+            by_shape.setdefault((tuple(w.shape), w.device), []).append(i)
+        else:
+            res[i] = quantize_weight(w, a, out_fmt)
+    for idx in by_shape.values():
+        for s in range(0, len(idx), 65535):
+            part = idx[s:s + 65535]
+            outs = GroupedQuantize([ws[i] for i in part], a, out_fmt).run()
+            for i, o in zip(part, outs):
+                res[i] = o
+    return res  # type: ignore[return-value]
 
 
 def fake_quantize(w: torch.Tensor, a: QuantizationArgs, col_scales: Optional[torch.Tensor] = None,
@@ -472,23 +559,28 @@ class PreparedQuantize:
         if rc:
             _lib.check(rc, "qz_quantize")
 
-    def prepare_many(self, ws: Sequence[torch.Tensor]) -> Callable[..., None]:
+    def prepare_many(self, ws: Sequence[torch.Tensor],
+                     outs: Optional[Sequence[Dict[str, torch.Tensor]]] = None) -> Callable[..., None]:
         """Marshal a qz_quantize_many call over every weight of ``ws`` (same geometry as
-        ``w_like``) into the prepared outputs; the returned ``go(stream=None)`` enqueues one
-        launch per weight from ONE host call."""
+        ``w_like``) into the prepared outputs (or into ``outs[i]`` for weight i); the returned
+        ``go(stream=None)`` enqueues one launch per weight from ONE host call."""
         b, r, c, ld_r, ld_b = self.geom
         for w in ws:
             if _geom(w) != self.geom or not w.is_cuda:
                 raise ValueError("prepare_many: every weight needs the prepared geometry and a device")
         n = len(ws)
 
-        def arr(t):
-            return None if t is None else (ctypes.c_void_p * n)(*([t.data_ptr()] * n))
+        if outs is not None and len(outs) != n:
+            raise ValueError("prepare_many: one output dict per weight")
 
-        args = (n, (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws]), arr(self.out["codes"]),
-                arr(self.out["scale"]), arr(self.out.get("zero_point")), arr(self.out.get("global_scale")),
+        def arr(key):
+            ts = [self.out.get(key)] * n if outs is None else [o.get(key) for o in outs]
+            return None if ts[0] is None else (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+
+        args = (n, (ctypes.c_void_p * n)(*[w.data_ptr() for w in ws]), arr("codes"),
+                arr("scale"), arr("zero_point"), arr("global_scale"),
                 b, r, c, ld_r, ld_b, ctypes.byref(self.ca), self.out_fmt, _P(self.ws.data_ptr()), self.ws.numel())
-        keep = list(ws)  # the pointers stay valid while the closure lives
+        keep = list(ws) + list(outs or [])  # the pointers stay valid while the closure lives
 
         def go(stream=None) -> None:
             st = _P(stream.cuda_stream) if stream is not None else _stream()

@@ -78,11 +78,61 @@ def awq_main(paths, libs):
                   f"-> {nbytes / (v[len(v)//2] * 1e-6) / 1e9:7.0f} GB/s alg")
 
 
+def grouped_main(paths, libs):
+    """MODE=grouped: qz_quantize_grouped over K steps (int4 g128), each step its own output set
+    (distinct outputs: OUTS=0) or OUTS rotating output sets."""
+    dev = torch.device("cuda:0")
+    K = int(os.environ.get("K", 100))
+    nouts = int(os.environ.get("OUTS", 0)) or K
+    ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
+    a = _lib.QzArgs(4, 0, 1, 2, G, 0, 0, 0)
+    codes = [torch.empty(ROWS, COLS // 8, dtype=torch.int32, device=dev) for _ in range(nouts)]
+    scale = [torch.empty(ROWS, COLS // G, dtype=torch.bfloat16, device=dev) for _ in range(nouts)]
+    tab = torch.tensor([[ws[i % COPIES].data_ptr() for i in range(K)], [codes[i % nouts].data_ptr() for i in range(K)],
+                        [scale[i % nouts].data_ptr() for i in range(K)], [0] * K], dtype=torch.int64).reshape(-1).to(dev)
+    st = torch.cuda.current_stream()
+    sp = P(st.cuda_stream)
+    for lib in libs:
+        lib.qz_quantize_grouped.argtypes = [ctypes.c_int64, P, ctypes.c_int64, ctypes.c_int64,
+                                            ctypes.POINTER(_lib.QzArgs), ctypes.c_int32, P]
+
+    def run(lib):
+        assert lib.qz_quantize_grouped(K, P(tab.data_ptr()), ROWS, COLS, ctypes.byref(a), 0, sp) == 0
+
+    ref = None
+    for lib in libs:
+        run(lib)
+        torch.cuda.synchronize()
+        cur = codes[-1].clone()
+        if ref is None:
+            ref = cur
+        elif not torch.equal(ref, cur):
+            print(f"NOTE: {lib._name} output differs")
+    res = {p: [] for p in paths}
+    for rnd in range(int(os.environ.get("ROUNDS", 6))):
+        for p, lib in zip(paths, libs):
+            run(lib)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(3):
+                run(lib)
+            e1.record(st)
+            torch.cuda.synchronize()
+            res[p].append(e0.elapsed_time(e1) * 1e3 / (3 * K))
+    alg = ROWS * COLS * 2 + ROWS * COLS // 2 + ROWS * COLS // G * 2
+    for p in paths:
+        v = sorted(res[p])
+        print(f"grouped K={K} outs={nouts} {os.path.basename(p):22s} median {v[len(v)//2]:7.2f} us/weight  "
+              f"min {v[0]:7.2f} -> {alg / (v[len(v)//2] * 1e-6) / 1e9:7.0f} GB/s alg")
+
+
 def main():
     paths = sys.argv[1:]
     libs = [load(p) for p in paths]
     if os.environ.get("MODE") == "awq":
         return awq_main(paths, libs)
+    if os.environ.get("MODE") == "grouped":
+        return grouped_main(paths, libs)
     dev = torch.device("cuda:0")
     ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
     if KIND == "int":
@@ -105,6 +155,10 @@ def main():
         fmt = 3
         codes = torch.empty(ROWS, COLS // 2, dtype=torch.uint8, device=dev)
         scale = torch.empty(ROWS, COLS // 32, dtype=torch.uint8, device=dev)
+    # OUTS=n: rotate n distinct output sets (step i writes set i % n; 1 = one shared set)
+    nouts = int(os.environ.get("OUTS", 1))
+    codes_l = [codes] + [torch.empty_like(codes) for _ in range(nouts - 1)]
+    scale_l = [scale] + [torch.empty_like(scale) for _ in range(nouts - 1)]
     n = libs[0].qz_quantize_workspace_size(1, ROWS, COLS, ctypes.byref(a))
     wsp = torch.empty(n + 256, dtype=torch.uint8, device=dev)
     st = torch.cuda.current_stream()
@@ -113,7 +167,8 @@ def main():
 
     def run(lib, i):
         rc = lib.qz_quantize(P(ws[i % COPIES].data_ptr()), 1, ROWS, COLS, COLS, ROWS * COLS, ctypes.byref(a), fmt,
-                             P(codes.data_ptr()), P(scale.data_ptr()), P(0), P(0), P(wsp.data_ptr()), wsp.numel(), sp)
+                             P(codes_l[i % nouts].data_ptr()), P(scale_l[i % nouts].data_ptr()), P(0), P(0),
+                             P(wsp.data_ptr()), wsp.numel(), sp)
         assert rc == 0, rc
 
     for lib in libs:  # correctness: every variant gives identical bits

@@ -436,3 +436,52 @@ def test_quantize_many_equals_single_calls(cuda):
     prep.prepare_many(ws)()
     torch.cuda.synchronize()
     assert torch.equal(outs[0]["codes"].cpu(), ref[-1]["weight_packed"].cpu())
+
+
+@pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "int8_g64_sym", "fp8_g32", "mxfp4_g32"])
+def test_quantize_grouped_equals_single_calls(cuda, scheme):
+    """qz_quantize_grouped (n weights, ONE launch, per-weight pointer table) == quantize_weight per
+    weight, bit for bit, in the small-launch path (3 weights) and in the large-launch path
+    (nt loads, UNROLL 4 tiles: 9 x [4096, 4096] = 302 MB > 256 MiB)."""
+    a = {"int4_g128_sym": QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128),
+         "int4_g32_asym": QuantizationArgs(num_bits=4, type="int", symmetric=False, group_size=32),
+         "int8_g64_sym": QuantizationArgs(num_bits=8, type="int", symmetric=True, group_size=64),
+         "fp8_g32": QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32),
+         "mxfp4_g32": QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")}[scheme]
+    for n, (r, c) in ((3, (96, 1024)), (9, (4096, 4096))):
+        ws = [_edge_weight(r, c, a.group_size, seed=s).to(cuda) for s in range(n)]
+        ref = [ops.quantize_weight(w, a) for w in ws]
+        got = ops.GroupedQuantize(ws, a).run()
+        torch.cuda.synchronize()
+        for o, rf in zip(got, ref):
+            assert torch.equal(o["codes"].cpu(), rf["codes"].cpu())
+            assert torch.equal(o["scale"].cpu().view(torch.uint8), rf["scale"].cpu().view(torch.uint8))
+            if not a.symmetric:
+                assert torch.equal(o["zero_point"].cpu(), rf["zero_point"].cpu())
+        del ws, ref, got
+    # quantize_weights: grouped per shape + per-weight launches for the rest, same results
+    mix = [_edge_weight(64, 256, a.group_size, seed=7).to(cuda), _edge_weight(32, 512, a.group_size, seed=8).to(cuda),
+           _edge_weight(64, 256, a.group_size, seed=9).to(cuda)]
+    for o, w in zip(ops.quantize_weights(mix, a), mix):
+        rf = ops.quantize_weight(w, a)
+        assert torch.equal(o["codes"].cpu(), rf["codes"].cpu())
+
+
+def test_quantize_grouped_rejects(cuda):
+    import ctypes
+    nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16)
+    w = _edge_weight(32, 256, 16, seed=1).to(cuda)
+    with pytest.raises(ValueError):
+        ops.GroupedQuantize([w], nv)
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    lib = _lib.load()
+    tab = torch.zeros(4, dtype=torch.int64, device=cuda)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.qz_quantize_grouped(1, ctypes.c_void_p(tab.data_ptr()), 32, 256, ctypes.byref(nv.to_c()), 3,
+                                   st) == _lib.QZ_ERR_FORMAT
+    assert lib.qz_quantize_grouped(-1, ctypes.c_void_p(tab.data_ptr()), 32, 256, ctypes.byref(a.to_c()), 0,
+                                   st) == _lib.QZ_ERR_SHAPE
+    assert lib.qz_quantize_grouped(0, None, 32, 256, ctypes.byref(a.to_c()), 0, st) == 0
+    with pytest.raises(ValueError):  # output aliasing a weight
+        ops.GroupedQuantize([w], a, outs=[{"codes": w.view(torch.int32)[:, :32], "scale": w[:, :2],
+                                           "zero_point": None}])
