@@ -357,21 +357,19 @@ def main():
     # pairs: step i reads copy i % COPIES and writes its own codes/scales (K distinct output
     # sets, so no two steps of the launch write the same bytes).
     grouped = not (args.per_weight_launch or args.python_loop or args.graph)
+    # everything is marshalled BEFORE the warmup, so each timed region directly follows its own
+    # W warmup steps (the card's clocks depend on the preceding ~ms of load: scripts/idle_gap.py)
+    outs_k = [{"codes": torch.empty_like(bufs["codes"]), "scale": torch.empty_like(bufs["scale"]),
+               "zero_point": None} for _ in range(args.steps)]
     if grouped:
-        def outs_for(n):
-            return [{"codes": torch.empty_like(bufs["codes"]), "scale": torch.empty_like(bufs["scale"]),
-                     "zero_point": None} for _ in range(n)]
         # (--profile-only: the warmup launch has the timed launch's size, so every launch of the
         # grouped kernel in a rocprofv3 pass covers K weights)
         nw = args.steps if args.profile_only else max(args.warmup, 1)
-        warm = ops.GroupedQuantize([copies[i % args.copies] for i in range(nw)], a, outs=outs_for(nw))
-        gq = ops.GroupedQuantize([copies[i % args.copies] for i in range(args.steps)], a,
-                                 outs=outs_for(args.steps))
-        warm.run(stream)  # W warmup steps (one grouped launch)
-        del warm
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize()
+        warm = ops.GroupedQuantize([copies[i % args.copies] for i in range(nw)], a,
+                                   outs=[{"codes": torch.empty_like(bufs["codes"]),
+                                          "scale": torch.empty_like(bufs["scale"]), "zero_point": None}
+                                         for _ in range(nw)])
+        gq = ops.GroupedQuantize([copies[i % args.copies] for i in range(args.steps)], a, outs=outs_k)
 
     # --graph: the K timed steps captured once into a hipGraph and replayed with one host call.
     # Measured on MI355X: kernels inside the replay run 25.4 us vs 21.0 us launched on the stream
@@ -389,10 +387,10 @@ def main():
         torch.cuda.synchronize()
 
     # One launch per weight: qz_quantize_many -- one host call that enqueues the K qz_quantize
-    # launches (each over its own resident copy, shared outputs) -- so the ~20 us Python/ctypes
-    # cost per call cannot leave the GPU idle between the ~21 us kernels.
+    # launches (each over its own resident copy, into the K distinct output sets) -- so the ~20 us
+    # Python/ctypes cost per call cannot leave the GPU idle between the ~21 us kernels.
     many = None if (graph is not None or args.python_loop) else \
-        prep.prepare_many([copies[i % args.copies] for i in range(args.steps)])
+        prep.prepare_many([copies[i % args.copies] for i in range(args.steps)], outs=outs_k)
 
     def run_steps(grouped_launch=grouped):
         if grouped_launch:
@@ -405,7 +403,15 @@ def main():
             for i in range(args.steps):
                 step(i)
 
+    def warmup(grouped_launch):
+        if grouped_launch:
+            warm.run(stream)  # W warmup steps (one grouped launch)
+        else:
+            for i in range(args.warmup):
+                step(i)
+
     if args.profile_only:
+        warmup(grouped)
         run_steps()
         torch.cuda.synchronize()
         return
@@ -433,15 +439,17 @@ def main():
     # ---- contract timing.  HIP events on the launch stream bracket the same region: for the
     # grouped launch their elapsed time IS the kernel's launch duration; for per-weight launches
     # elapsed / K is the average launch duration (back-to-back, no host gaps).
+    warmup(grouped)
     el, region_ms = timed_region(grouped)
     n_launches = 1 if grouped else args.steps
     k_ms_mean = region_ms / n_launches
 
-    # ---- secondary: one launch per weight (qz_quantize_many), same K steps, and one event pair
-    # around each launch (adds the event packets' ~1-2 us per launch)
+    # ---- secondary: one launch per weight (qz_quantize_many), same K steps into the same K
+    # distinct output sets, after its own W warmup steps; then one event pair around each launch
+    # (adds the event packets' ~1-2 us per launch)
     per_weight = None
-    if grouped:  # the same K steps into the same K distinct output sets, one launch per step
-        many = prep.prepare_many([copies[i % args.copies] for i in range(args.steps)], outs=gq.outs)
+    if grouped:
+        warmup(False)
         pw_el, pw_region_ms = timed_region(False)
         pw_us = pw_region_ms / args.steps * 1e3
         per_weight = {"kernel": KERNEL_NAME_SINGLE, "us_per_launch": pw_us,
@@ -449,7 +457,7 @@ def main():
                       "achieved_GBps": ALG_BYTES / (pw_us * 1e-6) / 1e9,
                       "frac": ALG_BYTES / (pw_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
                       "timing": "HIP events around K back-to-back qz_quantize launches (one qz_quantize_many call, "
-                                "the K distinct output sets of the grouped launch) / K"}
+                                "the K distinct output sets of the grouped launch) / K, after W warmup launches"}
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     for i in range(args.steps):
@@ -468,13 +476,15 @@ def main():
     measured = None
     if rank == 0:
         last = (args.steps - 1) % args.copies
-        o_last = gq.outs[args.steps - 1] if grouped else bufs
+        o_last = outs_k[args.steps - 1] if (grouped or many is not None) else bufs
         measured = (copies[last][:256].cpu(), o_last["codes"][:256].cpu(), o_last["scale"][:256].cpu())
         if grouped:  # the per-step event-pair launches wrote bufs from the same copy: must agree too
             measured = measured + (bufs["codes"][:256].cpu(), bufs["scale"][:256].cpu())
+    many_used = many is not None
     if grouped:
-        del gq
-        torch.cuda.empty_cache()
+        del gq, warm
+    del outs_k, many
+    torch.cuda.empty_cache()
 
     # ---- reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
     allgather = None
@@ -567,7 +577,7 @@ def main():
                                            "(qz_quantize_grouped) of the K steps" if grouped else
                                            "HIP events around the K back-to-back launches of the timed region / K"
                                            + (" (one hipGraph replay)" if graph is not None else
-                                              " (one qz_quantize_many call)" if many is not None else
+                                              " (one qz_quantize_many call)" if many_used else
                                               " (Python loop of qz_quantize calls)")),
                          "alg_bytes_per_launch": ALG_BYTES * per_launch,
                          "alg_bytes_per_weight": ALG_BYTES, "traffic_source": tsrc},

@@ -1283,8 +1283,11 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
   const bool nt = n * rows * cols * 2 > QZ_NT_BYTES_Q;
   const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(false, nt) * WAVE);
   const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
+#ifndef QZ_GRP_DYN_LDS
+#define QZ_GRP_DYN_LDS 0  // tuning knob: dynamic LDS per workgroup (caps occupancy)
+#endif
   hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, nt, true), dim3((unsigned)blocks, (unsigned)n),
-                     dim3(FBLOCK), 0, (hipStream_t)stream, F);
+                     dim3(FBLOCK), QZ_GRP_DYN_LDS, (hipStream_t)stream, F);
   return launch_err();
 }
 
