@@ -79,20 +79,27 @@ __global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, i
   for (int64_t t = t0; t < t1; ++t) acc += fabsf(bf2f(x[t * ld + c]));
   part[(int64_t)blockIdx.y * C + c] = acc;
 }
-// stage 2: block = 64 channels x 4 chunk lanes; lane sums chunks w, w+4, ... (fixed order),
-// the 4 lane sums are added in a fixed order; accumulated into sum[c]
-__global__ __launch_bounds__(256) void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
-  __shared__ float red[4][64];
+// stage 2: block = 64 channels x FW waves; wave w sums chunks w, w+FW, ... (fixed order, loads
+// unrolled so a lane has its chunks in flight together: the stage is latency-bound, ~nch*C*4 B),
+// the FW wave sums are added in a fixed order; accumulated into sum[c]
+constexpr int FW = 16;
+__global__ __launch_bounds__(FW * 64) void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
+  __shared__ float red[FW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   float acc = 0.f;
   if (c < C) {
-#pragma unroll 4
-    for (int64_t k = wv; k < nch; k += 4) acc += part[k * C + c];
+#pragma unroll 8
+    for (int64_t k = wv; k < nch; k += FW) acc += part[k * C + c];
   }
   red[wv][lane] = acc;
   __syncthreads();
-  if (wv == 0 && c < C) sum[c] += ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+  if (wv == 0 && c < C) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < FW; ++w) t += red[w][lane];
+    sum[c] += t;
+  }
 }
 
 // ----------------------------------------------- a5: grid-search loss sum((a - b)^2)
@@ -154,10 +161,17 @@ int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
   return std::max<int64_t>(1, std::min<int64_t>(2048, cdiv(rows * cols, 256 * 8 * 4)));
 }
 
+#ifndef QZ_ABSMEAN_MIN_TC
+#define QZ_ABSMEAN_MIN_TC 128  // tuning knob: minimum tokens per stage-1 chunk
+#endif
+#ifndef QZ_ABSMEAN_BLOCKS
+#define QZ_ABSMEAN_BLOCKS 2048  // tuning knob: target stage-1 workgroups
+#endif
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
-  // >= 128 tokens per chunk (32 per wave: one round of 8 loads); about 2048 stage-1 blocks
+  // >= QZ_ABSMEAN_MIN_TC tokens per chunk (32 per wave: one round of 8 loads); about
+  // QZ_ABSMEAN_BLOCKS stage-1 blocks
   const int64_t bx = cdiv(C, 512);
-  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, 128), cdiv(2048, bx)));
+  int64_t nch = std::max<int64_t>(1, std::min<int64_t>(cdiv(T, QZ_ABSMEAN_MIN_TC), cdiv(QZ_ABSMEAN_BLOCKS, bx)));
   *tc = cdiv(T, nch);
   return cdiv(T, *tc);
 }
@@ -339,7 +353,7 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   }
   int rc = launch_err();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 64)), dim3(256), 0, st, part, nch, channels, sum);
+  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 64)), dim3(FW * 64), 0, st, part, nch, channels, sum);
   return launch_err();
 }
 
