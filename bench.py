@@ -1,17 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark of the north-star kernel: int4 symmetric group-128 quantize + pack of a synthetic
-bf16 weight [11008, 4096] (BASELINE.json configs[1]: "Qwen3-4B AWQ int4 group_size=128 on
-1xMI355X"; metric "params quantized/sec + achieved HBM GB/s").
+"""Benchmark of the north-star path: int4 symmetric group-128 quantize + pack of every linear
+weight of a Qwen3-4B-shaped model (BASELINE.json configs[1], "Qwen3-4B AWQ int4 group_size=128 on
+1xMI355X"; metric "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128").
 
-One *step* = one fused quantize+pack pass over one [11008, 4096] bf16 weight already resident
-in HBM, into that step's own output tensors.  The step rotates over COPIES distinct input buffers
-(> the 256 MiB Infinity Cache) so every step streams its weight from HBM, not L3 (BASELINE.md
-timing protocol).  The K timed steps are ONE grouped launch (qz_quantize_grouped: grid.y = step,
-a device table of per-step weight/output pointers), the way the library quantizes many
-same-shape weights; the one-launch-per-weight rate (qz_quantize_many) is reported beside it
-(``per_weight_launch``), and ``--per-weight-launch`` makes it the timed path.  Multi-GPU: one process per GPU, each quantizes its own weight
-shard set (weak scaling, no collective in the timed region); after timing, ranks reassemble
-the packed tensors with one RCCL all-gather (reported separately, as the north star asks).
+One *step* = one pass of the product's compressor over the whole model: the 252 targeted
+linears (36 layers x q/k/v/o/gate/up/down, 3.63 G params, public Qwen3-4B dims, random bf16
+weights -- there is no checkpoint offline) quantized + packed by ``compressor.CompressionPlan``,
+the exact launch plan ``save_compressed`` runs (same-shape modules of one scheme in ONE grouped
+launch: 7 launches per step).  Weights (7.3 GB) and outputs (1.8 GB) stay resident in HBM, far
+larger than the 256 MiB Infinity Cache, so every step streams from HBM; the device->host copy
+that ``save_compressed`` adds is not in the timed region (DESIGN.md §6 gives the
+PCIe-inclusive rate).
+
+``value`` (params/s) and ``roofline.achieved`` come from the SAME timed region: wall clock
+(barrier + synchronize on both sides, max over ranks) for ``value``; HIP events on the launch
+stream around the same K steps for the kernel time (= the K x 7 launches back to back).  The
+rocprofv3 kernel trace of the same command is summarised by scripts/prof_summary.py.
+
+Beside it (not the headline): the north-star synthetic weight [11008, 4096] (grouped and one
+launch per weight), the AWQ kernels, a 2-layer AWQ oneshot, the other BASELINE configs, and the
+CPU baseline (the oracle's torch restatement on the host cores).  Multi-GPU: one process per GPU
+(torchrun), each quantizes its own model-sized weight set (weak scaling, no collective in the
+timed region); afterwards the ranks reassemble the compressed tensors with bucketed RCCL
+all-gathers (``distributed.gather_state``), timed separately.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -30,19 +41,15 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ROWS, COLS, GROUP, BITS = 11008, 4096, 128, 4
+ROWS, COLS, GROUP, BITS = 11008, 4096, 128, 4  # north-star synthetic weight (secondary leg)
 PARAMS = ROWS * COLS
-# algorithmic bytes per launch: read 2 B/param + packed 0.5 B/param + bf16 scale/group
+# algorithmic bytes per [11008, 4096] weight: read 2 B/param + packed 0.5 B/param
+# + one bf16 scale per group = 2.515625 B/param
 ALG_BYTES = PARAMS * 2 + PARAMS * BITS // 8 + (PARAMS // GROUP) * 2  # 113,426,432
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128"
-KERNEL_NAME_SINGLE = "k_group_fast<4, 0, false, true, false>"  # one launch per weight (90 MB < 256 MiB)
-NT_BYTES = 256 << 20  # QZ_NT_BYTES: launches reading more use nt loads + 4 KiB tiles
-
-
-def grouped_kernel_name(k):
-    nt = k * PARAMS * 2 > NT_BYTES
-    return f"k_group_fast<4, 0, false, true, {str(nt).lower()}, true>"
+RECIPE = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g128.yaml")
+MODEL_CFG = os.path.join(ROOT, "configs", "models", "qwen3-4b")
 
 # Qwen3-4B linear shapes (hidden 2560, inter 9728, 32 q / 8 kv heads x 128), 36 layers
 QWEN3_4B = [("q_proj", 4096, 2560), ("k_proj", 1024, 2560), ("v_proj", 1024, 2560), ("o_proj", 2560, 4096),
@@ -50,24 +57,69 @@ QWEN3_4B = [("q_proj", 4096, 2560), ("k_proj", 1024, 2560), ("v_proj", 1024, 256
 QWEN3_LAYERS = 36
 
 
+def kernel_name(grouped: bool, launch_weight_bytes: int, logl: int = 4, kind: int = 0, sym: bool = True) -> str:
+    """The k_group_fast instantiation a quantize launch runs, from the library's build constants
+    (qz_build_config): <LOGL, KIND, FQ, SYM, NT, GRP>; NT when the launch reads more than
+    nt_bytes_q."""
+    from quantizers_amd import _lib
+    nt = launch_weight_bytes > int(_lib.build_config()["nt_bytes_q"])
+    b = lambda v: str(bool(v)).lower()  # noqa: E731
+    return f"k_group_fast<{logl}, {kind}, false, {b(sym)}, {b(nt)}, {b(grouped)}>"
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=200)
-    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--copies", type=int, default=12)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-model-pass", action="store_true")
-    p.add_argument("--per-weight-launch", action="store_true",
-                   help="time one qz_quantize launch per step (qz_quantize_many) instead of one grouped launch")
-    p.add_argument("--python-loop", action="store_true",
-                   help="one Python qz_quantize call per step instead of one qz_quantize_many call")
-    p.add_argument("--graph", action="store_true",
-                   help="replay the K steps as one captured hipGraph (measured slower, see DESIGN.md §6)")
+    p.add_argument("--no-extras", action="store_true", help="headline only (no secondary legs)")
     p.add_argument("--profile-only", action="store_true",
-                   help="just warmup + K launches (for rocprofv3 runs); prints nothing else")
+                   help="warmup + K headline steps only (rocprofv3 PMC passes); prints nothing else")
     return p.parse_args()
+
+
+def cpu_baseline(seconds: float, checks=None):
+    """The oracle's torch restatement of compressed-tensors (oracle/ct_torch.py), timed on the host
+    cores on a bounded sample of the headline workload: repeated compress_weight calls on one
+    Qwen3-4B gate_proj-shaped weight [9728, 2560] (the model's largest shape class).  The oracle
+    is used only here (the CPU leg) and as the checker of ``checks`` = [(input rows, packed
+    codes, scales)] taken from the GPU's measured outputs (plain-C restatement, bit for bit).
+
+    Threads: 16 = the GPU box's CPU share for one GPU (its OMP_NUM_THREADS; gpurun sizes one
+    GPU's host share at 16 of the node's os.cpu_count() cores), not os.cpu_count() as BASELINE.md
+    §2 asks -- running 256 threads would take cores the box does not give one GPU's job."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ct_torch as ct  # CPU baseline leg only
+    import qref  # checker only
+    ok = None
+    if checks:
+        ok = True
+        for w_in, codes, scale in checks:
+            ref_p, ref_s = qref.int_sym_group_pack(w_in, BITS, GROUP)
+            ok = ok and bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    rows, cols = 9728, 2560
+    g = torch.Generator().manual_seed(0)
+    w = (torch.randn(rows, cols, generator=g) * 0.02).to(torch.bfloat16)
+    a = ct.QArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
+    ct.compress_weight(w, a)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ct.compress_weight(w, a)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 3) or n >= 2000:
+            break
+    res = {"value": n * rows * cols / el, "unit": "params/s", "cores": threads, "kind": "port",
+           "sample": f"oracle/ct_torch.compress_weight (compressed-tensors op sequence, torch CPU) int4-g{GROUP} on "
+                     f"one Qwen3-4B gate_proj-shaped bf16 weight [{rows},{cols}], {n} calls in {el:.1f}s, torch "
+                     f"threads={threads} (the box's per-GPU CPU share), os.cpu_count()={os.cpu_count()}, "
+                     f"cpu='{cpu_model()}'"}
+    return res, ok
 
 
 def cpu_model():
@@ -79,42 +131,6 @@ def cpu_model():
     except Exception:
         pass
     return platform.processor() or "unknown"
-
-
-def cpu_baseline(seconds: float, measured=None):
-    """The oracle's torch-op restatement of compressed-tensors (oracle/ct_torch.py), timed on the
-    host cores on the same synthetic weight.  The oracle is used only here (the
-    CPU leg): besides the timing it checks the GPU's measured output slices ``measured`` =
-    (input rows, packed codes, scales[, codes, scales of the per-weight launch]) bit for bit
-    against the plain-C restatement."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ct_torch as ct  # CPU baseline leg only
-    import qref  # checker only
-    ok = None
-    if measured is not None:
-        w_in, outs = measured[0], measured[1:]
-        ref_p, ref_s = qref.int_sym_group_pack(w_in, BITS, GROUP)
-        ok = all(bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
-                 for codes, scale in zip(outs[0::2], outs[1::2]))
-
-    threads = min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
-    torch.set_num_threads(threads)
-    g = torch.Generator().manual_seed(0)
-    w = (torch.randn(ROWS, COLS, generator=g) * 0.02).to(torch.bfloat16)
-    a = ct.QArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
-    ct.compress_weight(w, a)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
-        ct.compress_weight(w, a)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and n >= 3) or n >= 1000:
-            break
-    res = {"value": n * PARAMS / el, "unit": "params/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/ct_torch.compress_weight (compressed-tensors op sequence, torch CPU) on the same "
-                      f"bf16 [{ROWS},{COLS}] int4-g{GROUP} weight, {n} calls in {el:.1f}s, "
-                      f"torch threads={threads}, os.cpu_count()={os.cpu_count()}, cpu='{cpu_model()}'"}
-    return res, ok
 
 
 def _timed(fn, reps=3):
@@ -304,18 +320,51 @@ def awq_oneshot_layers(dev, n_layers=2, n_seq=16, seq=2048):
             "projected_36_layers_s": t / n_layers * 36, "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
 
 
-def read_pmc_traffic(kernel, weights_per_launch):
-    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json: bytes per weight x the weights one launch processes), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if not d.get("kernel", "").startswith(kernel):
-            return None, None
-        return d["hbm_bytes_per_weight"] * weights_per_launch, d.get("source")
-    except Exception:
-        return None, None
+def build_model(dev):
+    """A Qwen3-4B-shaped causal LM (configs/models/qwen3-4b: public dims, 36 layers) with random
+    bf16 weights on ``dev``, its targeted modules resolved from the AWQ int4-g128 recipe exactly
+    as ``oneshot`` resolves them."""
+    from transformers import AutoConfig, AutoModelForCausalLM
+    from quantizers_amd.oneshot import resolve_schemes
+    from quantizers_amd.recipe import parse_recipe
+    cfg = AutoConfig.from_pretrained(MODEL_CFG)
+    with torch.device(dev):
+        model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    schemes = resolve_schemes(model, parse_recipe(RECIPE))
+    model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
+    return model
+
+
+def synthetic_leg(ops, QuantizationArgs, dev, gen, stream, copies_n, k):
+    """North-star synthetic weight [11008, 4096] int4-g128: K weights (rotating over ``copies_n``
+    HBM-resident copies, 1.08 GB) into K distinct output sets, as ONE grouped launch and as K
+    per-weight launches (qz_quantize_many), each after its own warmup, HIP-event timed."""
+    a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
+    copies = [(torch.randn(ROWS, COLS, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+              for _ in range(copies_n)]
+    ws = [copies[i % copies_n] for i in range(k)]
+    outs = [ops.alloc_outputs((ROWS, COLS), a, None, dev) for _ in range(k)]
+    gq = ops.GroupedQuantize(ws, a, outs=outs)
+    prep = ops.PreparedQuantize(copies[0], a, ops.alloc_outputs((ROWS, COLS), a, None, dev))
+    many = prep.prepare_many(ws, outs=outs)
+    res = {}
+    for name, fn, launches in (("grouped", lambda: gq.run(stream), 1), ("per_weight", lambda: many(stream), k)):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us_w = e0.elapsed_time(e1) * 1e3 / k
+        gbps = ALG_BYTES / (us_w * 1e-6) / 1e9
+        res[name] = {"kernel": kernel_name(name == "grouped", (k if name == "grouped" else 1) * PARAMS * 2),
+                     "weights": k, "launches": launches, "us_per_weight": us_w, "params_per_s": PARAMS / (us_w * 1e-6),
+                     "achieved_GBps": gbps, "frac": gbps / HBM_PEAK_GBS}
+    check = (copies[(k - 1) % copies_n][:256].cpu(), outs[k - 1]["codes"][:256].cpu(), outs[k - 1]["scale"][:256].cpu())
+    del gq, many, prep, outs, ws
+    return res, copies, check
 
 
 def main():
@@ -339,219 +388,105 @@ def main():
     torch.cuda.set_device(dev)
 
     from quantizers_amd import ops
+    from quantizers_amd.compressor import CompressionPlan, compression_units
     from quantizers_amd.quantization import QuantizationArgs
 
-    a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
-    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    copies = [(torch.randn(ROWS, COLS, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
-              for _ in range(args.copies)]
-    out = ops.quantize_weight(copies[0], a)  # allocates outputs + workspace
-    bufs = {"codes": out["codes"], "scale": out["scale"], "zero_point": out["zero_point"]}
+    torch.manual_seed(1234 + rank)
+    model = build_model(dev)
+    units, _ = compression_units(model)
+    plan = CompressionPlan(units, dev)  # every pointer table / output built before timing
     stream = torch.cuda.current_stream(dev)
-    prep = ops.PreparedQuantize(copies[0], a, bufs)
+    params_step = plan.params
+    alg_step = plan.alg_bytes()
+    launches_step = plan.launches
 
-    def step(i, st=stream):
-        prep.run(copies[i % args.copies], st)
-
-    # Default: the K steps are ONE grouped launch (qz_quantize_grouped) over K (weight, outputs)
-    # pairs: step i reads copy i % COPIES and writes its own codes/scales (K distinct output
-    # sets, so no two steps of the launch write the same bytes).
-    grouped = not (args.per_weight_launch or args.python_loop or args.graph)
-    # everything is marshalled BEFORE the warmup, so each timed region directly follows its own
-    # W warmup steps (the card's clocks depend on the preceding ~ms of load: scripts/idle_gap.py)
-    outs_k = [{"codes": torch.empty_like(bufs["codes"]), "scale": torch.empty_like(bufs["scale"]),
-               "zero_point": None} for _ in range(args.steps)]
-    if grouped:
-        # (--profile-only: the warmup launch has the timed launch's size, so every launch of the
-        # grouped kernel in a rocprofv3 pass covers K weights)
-        nw = args.steps if args.profile_only else max(args.warmup, 1)
-        warm = ops.GroupedQuantize([copies[i % args.copies] for i in range(nw)], a,
-                                   outs=[{"codes": torch.empty_like(bufs["codes"]),
-                                          "scale": torch.empty_like(bufs["scale"]), "zero_point": None}
-                                         for _ in range(nw)])
-        gq = ops.GroupedQuantize([copies[i % args.copies] for i in range(args.steps)], a, outs=outs_k)
-
-    # --graph: the K timed steps captured once into a hipGraph and replayed with one host call.
-    # Measured on MI355X: kernels inside the replay run 25.4 us vs 21.0 us launched on the stream
-    # (per-node release fences), and the stream launches already run back to back (median gap 0).
-    graph = None
-    if args.graph:
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream(dev)
-        cap.wait_stream(stream)
-        with torch.cuda.graph(graph, stream=cap):
-            for i in range(args.steps):
-                step(i, torch.cuda.current_stream(dev))
-        stream.wait_stream(cap)
-        graph.replay()  # untimed: first replay uploads the graph
-        torch.cuda.synchronize()
-
-    # One launch per weight: qz_quantize_many -- one host call that enqueues the K qz_quantize
-    # launches (each over its own resident copy, into the K distinct output sets) -- so the ~20 us
-    # Python/ctypes cost per call cannot leave the GPU idle between the ~21 us kernels.
-    many = None if (graph is not None or args.python_loop) else \
-        prep.prepare_many([copies[i % args.copies] for i in range(args.steps)], outs=outs_k)
-
-    def run_steps(grouped_launch=grouped):
-        if grouped_launch:
-            gq.run(stream)
-        elif graph is not None:
-            graph.replay()
-        elif many is not None:
-            many(stream)
-        else:
-            for i in range(args.steps):
-                step(i)
-
-    def warmup(grouped_launch):
-        if grouped_launch:
-            warm.run(stream)  # W warmup steps (one grouped launch)
-        else:
-            for i in range(args.warmup):
-                step(i)
-
-    if args.profile_only:
-        warmup(grouped)
-        run_steps()
-        torch.cuda.synchronize()
-        return
-
-    def timed_region(grouped_launch):
-        """barrier + sync, exactly K steps, sync + barrier; wall seconds (max over ranks) and the
-        HIP-event time of the region on the launch stream (ms)."""
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    def region(k):
+        """barrier + sync, exactly k steps, sync + barrier: (wall s max over ranks, event ms)."""
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ev0.record(stream)
-        run_steps(grouped_launch)
-        ev1.record(stream)
+        e0.record(stream)
+        for _ in range(k):
+            plan.run(stream)
+        e1.record(stream)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        wall = time.perf_counter() - t0
-        t = torch.tensor([wall], device=dev, dtype=torch.float64)
+        wall = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
         if world > 1:
-            _all_reduce_max(t)
-        return t.item(), ev0.elapsed_time(ev1)
+            _all_reduce_max(wall)
+        return wall.item(), e0.elapsed_time(e1)
 
-    # ---- contract timing.  HIP events on the launch stream bracket the same region: for the
-    # grouped launch their elapsed time IS the kernel's launch duration; for per-weight launches
-    # elapsed / K is the average launch duration (back-to-back, no host gaps).
-    warmup(grouped)
-    el, region_ms = timed_region(grouped)
-    n_launches = 1 if grouped else args.steps
-    k_ms_mean = region_ms / n_launches
+    for _ in range(args.warmup):
+        plan.run(stream)
+    el, ev_ms = region(args.steps)
+    if args.profile_only:
+        return
 
-    # ---- secondary: one launch per weight (qz_quantize_many), same K steps into the same K
-    # distinct output sets, after its own W warmup steps; then one event pair around each launch
-    # (adds the event packets' ~1-2 us per launch)
-    per_weight = None
-    if grouped:
-        warmup(False)
-        pw_el, pw_region_ms = timed_region(False)
-        pw_us = pw_region_ms / args.steps * 1e3
-        per_weight = {"kernel": KERNEL_NAME_SINGLE, "us_per_launch": pw_us,
-                      "params_per_s": world * PARAMS * args.steps / pw_el,
-                      "achieved_GBps": ALG_BYTES / (pw_us * 1e-6) / 1e9,
-                      "frac": ALG_BYTES / (pw_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                      "timing": "HIP events around K back-to-back qz_quantize launches (one qz_quantize_many call, "
-                                "the K distinct output sets of the grouped launch) / K, after W warmup launches"}
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    for i in range(args.steps):
-        starts[i].record(stream)
-        step(i)
-        ends[i].record(stream)
-    torch.cuda.synchronize()
-    durs = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
-    if per_weight is not None:
-        per_weight["us_per_launch_events_mean"] = sum(durs) / len(durs) * 1e3
-        per_weight["us_per_launch_events_median"] = durs[len(durs) // 2] * 1e3
-    k_ms_each_mean = sum(durs) / len(durs)
-    k_ms_each_med = durs[len(durs) // 2]
+    # per-launch durations of one extra (untimed) step, one event pair per launch
+    per_launch = []
+    for gq, part, *_ in plan.grouped:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        gq.run(stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
+                                                         for t in o.values() if t is not None)
+        us = e0.elapsed_time(e1) * 1e3
+        per_launch.append({"shape": [gq.rows, gq.cols], "weights": gq.n, "us": us, "alg_bytes": nb,
+                           "GBps": nb / (us * 1e-6) / 1e9})
 
-    # ---- the measured buffers' first 256 rows, checked against the oracle in the CPU leg below
-    measured = None
-    if rank == 0:
-        last = (args.steps - 1) % args.copies
-        o_last = outs_k[args.steps - 1] if (grouped or many is not None) else bufs
-        measured = (copies[last][:256].cpu(), o_last["codes"][:256].cpu(), o_last["scale"][:256].cpu())
-        if grouped:  # the per-step event-pair launches wrote bufs from the same copy: must agree too
-            measured = measured + (bufs["codes"][:256].cpu(), bufs["scale"][:256].cpu())
-    many_used = many is not None
-    if grouped:
-        del gq, warm
-    del outs_k, many
-    torch.cuda.empty_cache()
+    checks = []
+    if rank == 0:  # the measured outputs of one module per shape, checked in the CPU leg
+        for gq, part, *_ in plan.grouped:
+            w = part[0][1]
+            checks.append((w[:64].cpu(), gq.outs[0]["codes"][:64].cpu(), gq.outs[0]["scale"][:64].cpu()))
 
-    # ---- reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
+    # reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
     allgather = None
     if world > 1:
-        gathered_codes = torch.empty((world,) + tuple(bufs["codes"].shape), dtype=bufs["codes"].dtype, device=dev)
-        gathered_scale = torch.empty((world,) + tuple(bufs["scale"].shape), dtype=bufs["scale"].dtype, device=dev)
-        for _ in range(3):
-            _all_gather_into(gathered_codes, bufs["codes"])
-            _all_gather_into(gathered_scale, bufs["scale"])
+        from quantizers_amd.distributed import gather_state
+        local_t = plan.tensors()
+        nbytes = sum(t.numel() * t.element_size() for t in local_t.values())
+        gather_state({f"r{rank}.{k}": v for k, v in local_t.items()})  # warm (communicator, buffers)
         torch.cuda.synchronize()
         dist.barrier()
         ta = time.perf_counter()
-        reps = 10
-        for _ in range(reps):
-            _all_gather_into(gathered_codes, bufs["codes"])
-            _all_gather_into(gathered_scale, bufs["scale"])
+        got = gather_state({f"r{rank}.{k}": v for k, v in local_t.items()})
         torch.cuda.synchronize()
-        allgather = (time.perf_counter() - ta) / reps * 1e3
+        dist.barrier()
+        allgather = {"ms": (time.perf_counter() - ta) * 1e3, "bytes_per_rank": nbytes,
+                     "tensors_gathered": len(got), "how": "distributed.gather_state: bucketed all_gather_into_tensor"}
+        del got, local_t
+    del plan, units, model
+    torch.cuda.empty_cache()
 
-    # ---- the AWQ kernels (a3-a6) on the same resident weights
-    awq = None
-    if not args.no_model_pass:
-        awq = awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream)
-
-    # ---- whole-model pass: every Qwen3-4B linear (36 layers, batched per shape)
-    model_pass = None
-    if not args.no_model_pass:
+    extras = {}
+    cpu_check = None
+    if not args.no_extras:
+        gen = torch.Generator(device=dev).manual_seed(99 + rank)
+        syn, copies, cpu_check = synthetic_leg(ops, QuantizationArgs, dev, gen, stream, args.copies, 100)
+        extras["north_star_synthetic_11008x4096"] = syn
+        extras["awq_kernels"] = awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream)
         del copies
         torch.cuda.empty_cache()
-        ws = []
-        for name, n, k in QWEN3_4B:
-            ws.append((name, (torch.randn(QWEN3_LAYERS, n, k, device=dev, generator=gen) * 0.02).to(torch.bfloat16)))
-        outs = [ops.quantize_weight(w, a) for _, w in ws]  # warm + allocate
-        torch.cuda.synchronize()
-        reps = 5
-        tm = time.perf_counter()
-        for _ in range(reps):
-            for (_, w), o in zip(ws, outs):
-                ops.quantize_weight(w, a, out={"codes": o["codes"], "scale": o["scale"], "zero_point": o["zero_point"]})
-        torch.cuda.synchronize()
-        mp = (time.perf_counter() - tm) / reps
-        nparams = sum(w.numel() for _, w in ws)
-        model_pass = {"params": nparams, "ms": mp * 1e3, "params_per_s": nparams / mp,
-                      "alg_GBps": nparams * (2 + BITS / 8 + 2 / GROUP) / mp / 1e9, "launches": len(ws)}
-
-    # ---- AWQ oneshot (scale search + smoothing) on a 2-layer Qwen3-4B, BASELINE configs[1]
-    awq_e2e = None
-    if not args.no_model_pass and world == 1:
-        awq_e2e = awq_oneshot_layers(dev)
-
-    # ---- the other BASELINE configs, one whole-model pass each (reported beside the headline)
-    other = None
-    if not args.no_model_pass:
+        if world == 1:
+            extras["awq_oneshot_qwen3_4b"] = awq_oneshot_layers(dev)
         other = other_configs(ops, QuantizationArgs, dev, gen)
         other["minimax_m2_1_mixedprec_sharded"] = minimax_pass(ops, QuantizationArgs, dev, gen, world, rank)
+        extras["other_configs"] = other
 
     cpu, ok = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, ok = cpu_baseline(args.cpu_seconds, measured)
+        cpu, ok = cpu_baseline(args.cpu_seconds, checks + ([cpu_check] if cpu_check else []))
 
     if rank == 0:
-        ms_step = el / args.steps * 1e3
-        value = world * PARAMS * args.steps / el
-        per_launch = args.steps if grouped else 1  # weights one launch processes
-        kernel = grouped_kernel_name(args.steps) if grouped else KERNEL_NAME_SINGLE
-        achieved = ALG_BYTES * per_launch / (k_ms_mean * 1e-3) / 1e9
-        traffic, tsrc = read_pmc_traffic(kernel, per_launch)
+        value = world * params_step * args.steps / el
+        ev_s = ev_ms * 1e-3
+        achieved = alg_step * args.steps / ev_s / 1e9
         line = {
             "metric": METRIC,
             "value": value,
@@ -559,39 +494,35 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": ms_step,
+            "ms_per_step": el / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic: torch.randn*0.02 bf16 weights (no checkpoint); same shape as Qwen3-4B's 11008x4096",
-            "config": {"workload": f"int4 sym group_size={GROUP} quantize+pack (pack-quantized) of bf16 W[{ROWS},{COLS}]"
-                                   f", {args.copies} rotating HBM-resident copies",
-                       "rows": ROWS, "cols": COLS, "group_size": GROUP, "num_bits": BITS,
+            "data": "synthetic: random-init bf16 weights of the public Qwen3-4B dims (no checkpoint offline)",
+            "config": {"workload": "int4 sym group_size=128 quantize+pack (pack-quantized) of all 252 Qwen3-4B linears "
+                                   "per step via compressor.CompressionPlan (the save_compressed launch plan)",
+                       "model": "Qwen3-4B dims, 36 layers", "params_per_step": params_step,
+                       "group_size": GROUP, "num_bits": BITS, "recipe": "configs/recipes/awq_w4a16_g128.yaml",
                        "parallelism": f"weight-shard dp{world}"},
-            "hbm_GBps_step": world * ALG_BYTES * args.steps / el / 1e9,
+            "hbm_GBps_step": world * alg_step * args.steps / el / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel, "kernel_ms_mean": k_ms_mean, "weights_per_launch": per_launch,
-                         "kernel_timing": ("HIP events around the timed region = the one grouped launch "
-                                           "(qz_quantize_grouped) of the K steps" if grouped else
-                                           "HIP events around the K back-to-back launches of the timed region / K"
-                                           + (" (one hipGraph replay)" if graph is not None else
-                                              " (one qz_quantize_many call)" if many_used else
-                                              " (Python loop of qz_quantize calls)")),
-                         "alg_bytes_per_launch": ALG_BYTES * per_launch,
-                         "alg_bytes_per_weight": ALG_BYTES, "traffic_source": tsrc},
-            "per_weight_launch": per_weight if grouped else {
-                "kernel": KERNEL_NAME_SINGLE, "us_per_launch_events_mean": k_ms_each_mean * 1e3,
-                "us_per_launch_events_median": k_ms_each_med * 1e3},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": kernel_name(True, 36 * 9728 * 2560 * 2),
+                         "kernel_ms_mean": ev_ms / (args.steps * launches_step),
+                         "launches_per_step": launches_step, "alg_bytes_per_step": alg_step,
+                         "alg_bytes_per_launch": alg_step / launches_step,
+                         "kernel_timing": "HIP events on the launch stream around the same K steps as value "
+                                          "(K x launches_per_step grouped launches back to back) / launches",
+                         "event_ms_per_step": ev_ms / args.steps,
+                         "traffic_note": "per-launch HBM bytes from rocprofv3 PMC passes: profiles/ (pmc_*), "
+                                         "see DESIGN.md §6"},
+            "per_launch": per_launch,
             "cpu_baseline": cpu,
             "parity_check": ok,
-            "allgather_ms": allgather,
-            "qwen3_4b_all_linears": model_pass,
-            "awq_kernels": awq,
-            "awq_oneshot_qwen3_4b": awq_e2e,
-            "other_configs": other,
+            "allgather": allgather,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

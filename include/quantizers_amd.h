@@ -79,6 +79,11 @@ enum {
 
 const char* qz_strerror(int code);
 int qz_version(void); /* MAJOR*10000 + MINOR*100 + PATCH */
+/* Compile-time tuning constants of this build ("key=value;..."; e.g. nt_bytes_q = weight bytes
+ * per quantize launch above which the group path streams non-temporally).  Benchmarks and
+ * profiles derive the kernel instantiation names they report from it.  No reference
+ * counterpart (build metadata). */
+const char* qz_build_config(void);
 
 /* Bytes of device workspace qz_quantize / qz_fake_quantize need for these args (0 for the
  * single-pass group path).  The workspace needs no initialisation. */

@@ -23,7 +23,7 @@ QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT, QZ_ERR_WORKSPACE, QZ_ERR_ALIGN = 
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = (
-    "qz_strerror", "qz_version", "qz_quantize_workspace_size", "qz_quantize", "qz_quantize_qparams",
+    "qz_strerror", "qz_version", "qz_build_config", "qz_quantize_workspace_size", "qz_quantize", "qz_quantize_qparams",
     "qz_observe_minmax", "qz_calculate_qparams", "qz_dequantize", "qz_pack_int32",
     "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_accum",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
@@ -59,6 +59,7 @@ def load() -> ctypes.CDLL:
     sig = {
         "qz_strerror": ([ctypes.c_int], ctypes.c_char_p),
         "qz_version": ([], ctypes.c_int),
+        "qz_build_config": ([], ctypes.c_char_p),
         "qz_quantize_workspace_size": ([I64, I64, I64, A], SZ),
         "qz_quantize": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P, SZ, P], ctypes.c_int),
         "qz_quantize_many": ([I64, P, P, P, P, P, I64, I64, I64, I64, I64, A, I32, P, SZ, P], ctypes.c_int),
@@ -86,6 +87,15 @@ def load() -> ctypes.CDLL:
         fn.restype = restype
     _lib = lib
     return lib
+
+
+def build_config() -> dict:
+    """The library's compile-time tuning constants (qz_build_config) as a dict."""
+    out = {}
+    for kv in load().qz_build_config().decode().split(";"):
+        k, _, v = kv.partition("=")
+        out[k] = int(v) if v.lstrip("-").isdigit() else v
+    return out
 
 
 _VALUE_ERRORS = {QZ_ERR_SHAPE, QZ_ERR_GROUP, QZ_ERR_BLOCK, QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT,

@@ -1,8 +1,10 @@
 """compressed-tensors checkpoint writer / reader.
 
 Replaces ``model.save_pretrained(output_dir, save_compressed=True)`` (scripts/do_oneshot.py:197):
-every targeted weight is quantized + packed on the GPU by the fused kernel (ops.compress_weight;
-fused-expert slices of one parameter in a single batched launch) and written under the
+every targeted weight is quantized + packed on the GPU by the fused kernel (``CompressionPlan``:
+same-shape dense modules of one scheme in ONE grouped launch, fused-expert slices of one
+parameter in a single batched launch; results copied to pinned host memory asynchronously) and
+written under the
 compressed-tensors names the reference itself pins in
 scripts/recombine_weights_MiniMax-M2.1.py:54-65 (``weight_packed``, ``weight_scale``,
 ``weight_shape``, ``weight_zero_point``; ``weight`` for float-quantized; plus
@@ -14,14 +16,16 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict, List, Optional
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
+import torch.distributed as dist
 from safetensors.torch import load_file, save_file
 from torch import nn
 
 from . import ops
-from .model import batch_groups, checkpoint_name, iter_linears, model_type, stacked_view
+from .model import LinearRef, batch_groups, checkpoint_name, iter_linears, model_type, stacked_view
 from .quantization import QuantizationArgs, QuantizationScheme, compression_format
 
 CT_VERSION = "0.13.1.dev0+quantizers_amd"  # format revision written (reference run: recombine...py:133)
@@ -64,50 +68,49 @@ def quantization_config_for(scheme_map: Dict[str, QuantizationScheme], linear_na
             "sparsity_config": {}, "transform_config": {}, "version": CT_VERSION}
 
 
-@torch.no_grad()
-def compressed_state_dict(model: nn.Module, device=None) -> Dict[str, torch.Tensor]:
-    """All tensors to write: compressed targeted weights + untouched parameters/buffers."""
+# ------------------------------------------------------------------ compression units / plan
+@dataclass
+class CompressUnit:
+    """One compressor work item: a dense Linear weight, or the same-shaped slices of one fused
+    expert parameter (``stacked``: one batched launch over ``[E, rows, cols]``)."""
+
+    refs: List[LinearRef]
+    scheme: QuantizationScheme
+    stacked: bool
+
+    def view(self) -> torch.Tensor:
+        w = stacked_view(self.refs)
+        return w if self.stacked else w[0]
+
+    @property
+    def nbytes(self) -> int:
+        return sum(r.weight.numel() for r in self.refs) * 2
+
+
+def compression_units(model: nn.Module) -> Tuple[List[CompressUnit], Dict[str, torch.Tensor]]:
+    """The targeted weights as compression units, and every tensor written unchanged (unquantized
+    fused-expert slices, biases of quantized Linears, all other parameters and buffers), keyed by
+    checkpoint name."""
     scheme_map: Dict[str, QuantizationScheme] = getattr(model, "quantization_scheme_map", {})
-    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     refs = iter_linears(model)
-    out: Dict[str, torch.Tensor] = {}
-    replaced_params = set()  # id() of parameters whose content is written per module
+    units: List[CompressUnit] = []
+    raw: Dict[str, torch.Tensor] = {}
+    replaced_params = set()  # id() of fused parameters whose content is written per expert
     for group in batch_groups(refs):
         r0 = group[0]
-        p = getattr(r0.module, r0.param_name)
         if r0.index is not None:
-            replaced_params.add(id(p))
-        q = [g for g in group if g.name in scheme_map]
-        if not q:
-            if r0.index is not None:  # unquantized fused expert slices: per-expert `.weight`
-                for g in group:
-                    out[f"{g.name}.weight"] = g.weight.detach().to("cpu").clone()
+            replaced_params.add(id(getattr(r0.module, r0.param_name)))
+        if r0.index is not None and all(g.name in scheme_map for g in group) \
+                and len({id(scheme_map[g.name]) for g in group}) == 1:
+            units.append(CompressUnit(list(group), scheme_map[r0.name], stacked=True))
             continue
-        if len(q) != len(group):  # mixed targets inside one fused group: compress one by one
-            subgroups = [[g] for g in group]
-        else:
-            subgroups = [group]
-        for sg in subgroups:
-            if sg[0].name not in scheme_map:
-                for g in sg:
-                    out[f"{g.name}.weight"] = g.weight.detach().to("cpu").clone()
-                continue
-            sch = scheme_map[sg[0].name]
-            w = stacked_view(sg).to(device)
-            if r0.index is None:
-                w = w[0]
-            comp = ops.compress_weight(w, sch.weights, has_activation_quant=sch.input_activations is not None)
-            for i, g in enumerate(sg):
-                for k, v in comp.items():
-                    if k == "weight_shape":
-                        out[f"{g.name}.{k}"] = v.clone()
-                    elif w.dim() == 3:
-                        out[f"{g.name}.{k}"] = v[i].detach().to("cpu").clone().reshape(
-                            v.shape[1:] if v.dim() > 1 else (1,))
-                    else:
-                        out[f"{g.name}.{k}"] = v.detach().to("cpu").clone()
-                if r0.index is None and g.bias is not None:
-                    out[f"{g.name}.bias"] = g.bias.detach().to("cpu").clone()
+        for g in group:  # dense Linear, or fused slices with mixed targets: one unit each
+            if g.name in scheme_map:
+                units.append(CompressUnit([g], scheme_map[g.name], stacked=False))
+                if g.index is None and g.bias is not None:
+                    raw[f"{g.name}.bias"] = g.bias.detach()
+            elif g.index is not None:
+                raw[f"{g.name}.weight"] = g.weight.detach()
     mtype = model_type(model)
     quant_linears = {g.name for g in refs if g.name in scheme_map and g.index is None}
     for name, prm in model.named_parameters():
@@ -117,19 +120,239 @@ def compressed_state_dict(model: nn.Module, device=None) -> Dict[str, torch.Tens
         mod_name, _, leaf = cname.rpartition(".")
         if mod_name in quant_linears and leaf in ("weight", "bias"):
             continue
-        if cname not in out:
-            out[cname] = prm.detach().to("cpu").clone()
+        raw.setdefault(cname, prm.detach())
     for name, buf in model.named_buffers():
         cname = checkpoint_name(name, mtype)
-        if cname not in out and not name.endswith("inv_freq"):
-            out[cname] = buf.detach().to("cpu").clone()
+        if cname not in raw and not name.endswith("inv_freq"):
+            raw[cname] = buf.detach()
+    return units, raw
+
+
+class CompressionPlan:
+    """Prepared kernel launches for a set of compression units whose weights are on ``device``
+    (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
+    grouped launch (``ops.GroupedQuantize``: the per-launch ramp paid once per shape, e.g. 7
+    launches for all 252 Qwen3-4B linears); stacked fused experts, FP8_BLOCK, NVFP4 and other
+    two-pass schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
+    friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
+
+    def __init__(self, units: Sequence[CompressUnit], device):
+        self.device = torch.device(device)
+        self.grouped = []  # (GroupedQuantize, [(unit, weight)], args, int_q, fmt)
+        self.singles = []  # (unit, weight, preallocated outputs, args, int_q, fmt)
+        buckets: Dict[tuple, list] = {}
+        self.params = 0
+        for u in units:
+            a = u.scheme.weights
+            w = u.view()
+            if w.device != self.device:
+                w = w.to(self.device)
+            self.params += w.numel()
+            int_q, fmt = ops._compress_plan(a, u.scheme.input_activations is not None)
+            if not u.stacked and ops.grouped_ok(a, w):
+                buckets.setdefault((id(u.scheme), tuple(w.shape)), []).append((u, w))
+            else:
+                self.singles.append((u, w, ops.alloc_outputs(tuple(w.shape), a, fmt, self.device), a, int_q, fmt))
+        for items in buckets.values():
+            a = items[0][0].scheme.weights
+            int_q, fmt = ops._compress_plan(a, items[0][0].scheme.input_activations is not None)
+            for s in range(0, len(items), 65535):
+                part = items[s:s + 65535]
+                gq = ops.GroupedQuantize([w for _, w in part], a, fmt)
+                self.grouped.append((gq, part, a, int_q, fmt))
+
+    @property
+    def launches(self) -> int:
+        return len(self.grouped) + len(self.singles)
+
+    def alg_bytes(self) -> int:
+        """Algorithmic HBM bytes of one run(): every weight read once + every output written once."""
+        n = self.params * 2
+        outs = [o for gq, *_ in self.grouped for o in gq.outs] + [o for _, _, o, *_ in self.singles]
+        for o in outs:
+            for t in o.values():
+                if t is not None:
+                    n += t.numel() * t.element_size()
+        return n
+
+    def run(self, stream=None) -> None:
+        for gq, *_ in self.grouped:
+            gq.run(stream)
+        if self.singles:
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device)):
+                for u, w, o, a, int_q, fmt in self.singles:
+                    ops.quantize_weight(w, a, out_fmt=fmt, out=o)
+
+    def tensors(self) -> Dict[str, torch.Tensor]:
+        """The on-disk tensors of every unit (device tensors; ``weight_shape`` on the host)."""
+        out: Dict[str, torch.Tensor] = {}
+        for gq, part, a, int_q, fmt in self.grouped:
+            for (u, w), q in zip(part, gq.outs):
+                for k, v in ops._compressed_tensors(q, tuple(w.shape), a, int_q, fmt).items():
+                    out[f"{u.refs[0].name}.{k}"] = v
+        for u, w, q, a, int_q, fmt in self.singles:
+            comp = ops._compressed_tensors(q, tuple(w.shape), a, int_q, fmt)
+            for i, g in enumerate(u.refs):
+                for k, v in comp.items():
+                    if k == "weight_shape":
+                        out[f"{g.name}.{k}"] = v.clone()  # one tensor per module (no shared storage)
+                    elif not u.stacked:
+                        out[f"{g.name}.{k}"] = v
+                    else:
+                        out[f"{g.name}.{k}"] = v[i].reshape(v.shape[1:] if v.dim() > 1 else (1,))
+        return out
+
+
+def _chunks(units: Sequence[CompressUnit], budget: int, device) -> List[List[CompressUnit]]:
+    """Split units so the weights staged on ``device`` per plan stay under ``budget`` bytes
+    (device-resident weights need no staging and form one plan)."""
+    out: List[List[CompressUnit]] = [[]]
+    size = 0
+    for u in units:
+        staged = u.refs[0].weight.device != torch.device(device)
+        nb = u.nbytes if staged else 0
+        if out[-1] and size + nb > budget:
+            out.append([])
+            size = 0
+        out[-1].append(u)
+        size += nb
+    return [c for c in out if c]
+
+
+class _HostCopier:
+    """Asynchronous device -> pinned-host copies on a side stream: the copies of one plan overlap
+    the next plan's kernels; at most ``budget`` bytes of device results are kept alive waiting
+    for their copies."""
+
+    def __init__(self, device, budget: int = 8 << 30):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device)
+        self.pending = []  # (done event, device tensors, bytes)
+        self.inflight = 0
+        self.budget = budget
+
+    def submit(self, items: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        dev_items = {k: t for k, t in items.items() if t.is_cuda}
+        host = {k: t for k, t in items.items() if not t.is_cuda}
+        if not dev_items:
+            return host
+        ready = torch.cuda.Event()
+        ready.record(torch.cuda.current_stream(self.device))
+        self.stream.wait_event(ready)
+        offs, total = {}, 0
+        for k, t in dev_items.items():
+            offs[k] = total
+            total += (t.numel() * t.element_size() + 63) // 64 * 64
+        buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
+        with torch.cuda.stream(self.stream):
+            for k, t in dev_items.items():
+                nb = t.numel() * t.element_size()
+                h = buf[offs[k]:offs[k] + nb].view(t.dtype).view(t.shape)
+                h.copy_(t.contiguous(), non_blocking=True)
+                host[k] = h
+        done = torch.cuda.Event()
+        done.record(self.stream)
+        self.pending.append((done, list(dev_items.values()), total))
+        self.inflight += total
+        while self.inflight > self.budget and len(self.pending) > 1:
+            self._retire()
+        return host
+
+    @property
+    def last_event(self):
+        """Completion event of the latest submit (None before the first device copy)."""
+        return self.pending[-1][0] if self.pending else None
+
+    def _retire(self):
+        done, _, nb = self.pending.pop(0)
+        done.synchronize()
+        self.inflight -= nb
+
+    def finish(self):
+        while self.pending:
+            self._retire()
+
+
+def _dist_info() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+STAGE_BYTES = 4 << 30  # host-resident weights staged on the device per plan
+
+
+@torch.no_grad()
+def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
+                          dst: Optional[int] = None) -> Dict[str, torch.Tensor]:
+    """All tensors to write: compressed targeted weights + untouched parameters/buffers.
+
+    One process: every unit is compressed by ``CompressionPlan`` (grouped launches) and copied
+    to pinned host memory asynchronously.  Under ``torch.distributed`` (one process per GPU, every
+    rank holding the same model): the units are assigned to ranks by bytes (LPT,
+    ``distributed.plan_shards``), each rank compresses its share with no collective on the data
+    path, and ``distributed.gather_state`` reassembles the compressed tensors with bucketed RCCL
+    all-gathers -- on every rank (``dst=None``) or only on rank ``dst`` (others get ``{}``)."""
+    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    units, raw = compression_units(model)
+    world, rank = _dist_info()
+    mine = units
+    if world > 1:
+        from .distributed import plan_shards
+        plan = plan_shards([(str(i), u.nbytes) for i, u in enumerate(units)], world)
+        keep = {int(k) for k in plan[rank]}
+        mine = [u for i, u in enumerate(units) if i in keep]
+    copier = _HostCopier(device) if (to_host and world == 1 and device.type == "cuda") else None
+    local: Dict[str, torch.Tensor] = {}
+    for chunk in _chunks(mine, STAGE_BYTES, device):
+        plan = CompressionPlan(chunk, device)
+        plan.run()
+        t = plan.tensors()
+        local.update(copier.submit(t) if copier is not None else t)
+        del plan
+    if copier is not None:
+        copier.finish()
+    receiver = world == 1 or dst is None or rank == dst
+    if world > 1:
+        from .distributed import gather_state
+        local = gather_state(local, dst=dst, to_host=to_host)
+    if not receiver:
+        return {}
+    out = dict(local)
+    dev_raw = {k: v for k, v in raw.items() if v.is_cuda}
+    if to_host:
+        if dev_raw:
+            copier = _HostCopier(device)
+            out.update(copier.submit(dev_raw))
+            copier.finish()
+        for k, v in raw.items():
+            if not v.is_cuda:
+                out[k] = v.clone()
+    else:
+        out.update(raw)
     return out
 
 
 def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SHARD_BYTES, device=None) -> str:
-    """Write safetensors shards + index + config.json(quantization_config)."""
+    """Write safetensors shards + index + config.json(quantization_config).  Under
+    ``torch.distributed`` the compression is sharded over the ranks (``compressed_state_dict``)
+    and rank 0 alone writes; every rank returns after the files exist."""
+    world, rank = _dist_info()
+    sd = compressed_state_dict(model, device, dst=0)
+    qcfg = quantization_config(model)
+    if hasattr(model, "config"):
+        # so a later model.config.save_pretrained(output_dir) keeps the compressed-tensors config
+        model.config.quantization_config = qcfg
+    if rank == 0:
+        _write_checkpoint(sd, model, qcfg, output_dir, max_shard_bytes)
+    if world > 1:
+        dist.barrier()
+    return output_dir
+
+
+def _write_checkpoint(sd: Dict[str, torch.Tensor], model: nn.Module, qcfg: dict, output_dir: str,
+                      max_shard_bytes: int) -> None:
     os.makedirs(output_dir, exist_ok=True)
-    sd = compressed_state_dict(model, device)
     names = sorted(sd)
     shards: List[Dict[str, torch.Tensor]] = [{}]
     size = 0
@@ -155,11 +378,10 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
         with open(os.path.join(output_dir, "model.safetensors.index.json"), "w") as f:
             json.dump({"metadata": {"total_size": total}, "weight_map": wmap}, f, indent=2)
     cfg = model.config.to_dict() if hasattr(model, "config") else {}
-    cfg["quantization_config"] = quantization_config(model)
+    cfg["quantization_config"] = qcfg
     with open(os.path.join(output_dir, "config.json"), "w") as f:
         json.dump(cfg, f, indent=2, default=str)
     _write_recipe(getattr(model, "quantization_recipe", None), output_dir)
-    return output_dir
 
 
 def _write_recipe(recipe, output_dir: str) -> None:

@@ -93,7 +93,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define QZ_HW_FP4 1
 #endif
 #ifndef QZ_NT_BYTES
-#define QZ_NT_BYTES (256ll << 20)  // fake-quant: weight bytes per launch above which loads are non-temporal
+#define QZ_NT_BYTES 268435456  // 256 MiB; fake-quant: weight bytes per launch above which loads are non-temporal
 #endif
 // quantize (+pack): weight bytes per launch above which the group path streams non-temporally
 // (nt loads + nt stores).  Measured with DISTINCT output tensors per weight, as a whole-model pass
@@ -1073,7 +1073,17 @@ const char* qz_strerror(int code) {
   return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
 }
 
-int qz_version(void) { return 100; }
+int qz_version(void) { return 200; }
+
+const char* qz_build_config(void) {
+#define QZ_STR2(x) #x
+#define QZ_STR(x) QZ_STR2(x)
+  return "nt_bytes_q=" QZ_STR(QZ_NT_BYTES_Q) ";nt_bytes_fq=" QZ_STR(QZ_NT_BYTES) ";unroll=" QZ_STR(QZ_UNROLL)
+         ";unroll_nt=" QZ_STR(QZ_UNROLL_NT) ";fast_block=" QZ_STR(QZ_FAST_BLOCK) ";reg_loads=" QZ_STR(QZ_REG_LOADS)
+         ";reg_loads_grp=" QZ_STR(QZ_REG_LOADS_GRP) ";arch=gfx950";
+#undef QZ_STR
+#undef QZ_STR2
+}
 
 size_t qz_quantize_workspace_size(int64_t batch, int64_t rows, int64_t cols, const qz_args* a) {
   Plan pl;

@@ -16,7 +16,7 @@ Works with backend "nccl" (RCCL, GPU tensors) and "gloo" (CPU tensors, used by t
 from __future__ import annotations
 
 import heapq
-from typing import Callable, Dict, List, Sequence, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -37,52 +37,89 @@ def plan_shards(items: Sequence[Item], world: int) -> List[List[str]]:
 
 
 def _flatten(tensors: Dict[str, torch.Tensor], device) -> Tuple[torch.Tensor, List[Tuple[str, str, Tuple[int, ...], int]]]:
+    """Pack ``tensors`` (sorted by name) into one uint8 buffer on ``device``, every tensor 16-B
+    aligned; returns the buffer and [(name, dtype, shape, byte offset)]."""
     meta = []
-    parts = []
     off = 0
     for k in sorted(tensors):
-        t = tensors[k].contiguous()
-        b = t.view(torch.uint8).reshape(-1) if t.numel() else torch.empty(0, dtype=torch.uint8, device=t.device)
+        t = tensors[k]
+        nb = t.numel() * t.element_size()
         meta.append((k, str(t.dtype).replace("torch.", ""), tuple(t.shape), off))
-        parts.append(b.to(device))
-        off += b.numel()
-        pad = (-off) % 16  # keep every tensor 16-B aligned inside the buffer (view(dtype))
-        if pad:
-            parts.append(torch.zeros(pad, dtype=torch.uint8, device=device))
-            off += pad
-    flat = torch.cat(parts) if parts else torch.empty(0, dtype=torch.uint8, device=device)
+        off += (nb + 15) // 16 * 16
+    flat = torch.zeros(off, dtype=torch.uint8, device=device)
+    for k, _, _, o in meta:
+        t = tensors[k].contiguous()
+        nb = t.numel() * t.element_size()
+        if nb:
+            flat[o:o + nb].copy_(t.reshape(-1).view(torch.uint8), non_blocking=True)
     return flat, meta
 
 
-def _unflatten(flat: torch.Tensor, meta) -> Dict[str, torch.Tensor]:
+def _unflatten(flat: torch.Tensor, meta, copy: bool = True) -> Dict[str, torch.Tensor]:
     out = {}
     for k, dt, shape, off in meta:
         dtype = getattr(torch, dt)
-        n = int(torch.tensor(shape).prod().item()) if shape else 1
+        n = 1
+        for d in shape:
+            n *= d
         nb = n * torch.empty((), dtype=dtype).element_size()
-        out[k] = flat[off:off + nb].view(dtype).reshape(shape).clone()
+        t = flat[off:off + nb].view(dtype).reshape(shape)
+        out[k] = t.clone() if copy else t
     return out
 
 
-def gather_state(local: Dict[str, torch.Tensor], device=None) -> Dict[str, torch.Tensor]:
-    """All ranks get the union of every rank's tensors (one all_gather_into_tensor)."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
-        return dict(local)
-    world = dist.get_world_size()
+GATHER_BUCKET_BYTES = 1 << 30  # bytes per rank per all-gather round
+
+
+def gather_state(local: Dict[str, torch.Tensor], device=None, dst: Optional[int] = None, to_host: bool = False,
+                 bucket_bytes: int = GATHER_BUCKET_BYTES) -> Dict[str, torch.Tensor]:
+    """Reassemble every rank's tensors: the union of all ranks' ``local`` dicts on every rank
+    (``dst=None``) or on rank ``dst`` only (the other ranks return ``{}``).
+
+    Each rank's tensors are packed into one flat byte buffer; the buffers (padded to the largest
+    rank's size) travel in rounds of ``bucket_bytes`` per rank, one ``all_gather_into_tensor``
+    per round -- a few large RCCL collectives over the point-to-point xGMI links rather than one
+    per tensor, with a bounded staging footprint.  ``to_host``: the receivers' results land in
+    pinned host memory (the writer's input), otherwise on ``device``."""
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    if world == 1:
+        if not to_host:
+            return dict(local)
+        return {k: (v.cpu() if v.is_cuda else v) for k, v in local.items()}
+    rank = dist.get_rank()
+    nccl = dist.get_backend() == "nccl"
     if device is None:
-        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+        device = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
     flat, meta = _flatten(local, device)
     metas: List = [None] * world
     dist.all_gather_object(metas, (flat.numel(), meta))
     maxn = max(m[0] for m in metas)
-    buf = torch.zeros(maxn, dtype=torch.uint8, device=device)
-    buf[: flat.numel()] = flat
-    allbuf = torch.empty(world * maxn, dtype=torch.uint8, device=device)
-    dist.all_gather_into_tensor(allbuf, buf)
+    receiver = dst is None or rank == dst
+    host_dev = torch.device("cpu") if to_host else torch.device(device)
+    pin = to_host and flat.is_cuda
+    dest = [torch.empty(metas[r][0], dtype=torch.uint8, device=host_dev, pin_memory=pin) for r in range(world)] \
+        if receiver else None
+    step = max(16, min(bucket_bytes, maxn) // 16 * 16) if maxn else 16
+    send = torch.zeros(step, dtype=torch.uint8, device=device)
+    recv = torch.empty(world * step, dtype=torch.uint8, device=device)
+    for off in range(0, maxn, step):
+        n = min(step, maxn - off)
+        valid = max(0, min(n, flat.numel() - off))
+        if valid:
+            send[:valid].copy_(flat[off:off + valid])
+        dist.all_gather_into_tensor(recv[: world * n], send[:n])
+        if receiver:
+            for r in range(world):
+                take = max(0, min(n, metas[r][0] - off))
+                if take:
+                    dest[r][off:off + take].copy_(recv[r * n: r * n + take], non_blocking=pin)
+    if not receiver:
+        return {}
+    if pin:
+        torch.cuda.current_stream(device).synchronize()
     out: Dict[str, torch.Tensor] = {}
     for r in range(world):
-        n, m = metas[r]
-        out.update(_unflatten(allbuf[r * maxn: r * maxn + n], m))
+        out.update(_unflatten(dest[r], metas[r][1], copy=False))
     return out
 
 

@@ -7,8 +7,9 @@ Every floating 2-D ``<module>.weight`` tensor whose module name is not matched b
 is a quantization target (a checkpoint has no module types; the reference's ignore list names
 the non-Linear 2-D tensors such as ``model.embed_tokens``).  Per shard file:
 
-  disk --(reader threads, mmap)--> host --H2D--> fused HIP quantize+pack (ops.compress_weight)
-       --D2H--> host --(writer threads)--> disk
+  disk --(reader threads, mmap)--> host --H2D--> fused HIP quantize+pack (ops.compress_weights:
+       the file's same-shape weights in one grouped launch) --async D2H, pinned--> host
+       --(writer threads, after the copy event)--> disk
 
 Reads of file i+1 and writes of file i-1 overlap the GPU work on file i.  Output shards keep
 the input file names; ``model.safetensors.index.json`` and ``config.json`` (with
@@ -37,7 +38,7 @@ from safetensors import safe_open
 from safetensors.torch import save_file
 
 from . import ops
-from .compressor import quantization_config_for
+from .compressor import _HostCopier, quantization_config_for
 from .distributed import plan_shards
 from .quantization import QuantizationArgs, QuantizationScheme, preset_scheme
 from .recipe import match_any
@@ -94,9 +95,15 @@ def _read(path: str) -> Dict[str, torch.Tensor]:
 
 
 def _quantize_file(tensors: Dict[str, torch.Tensor], sch: QuantizationScheme, ignore: List[str], device,
-                   quantized: List[str], skipped: List[str]) -> Dict[str, torch.Tensor]:
+                   quantized: List[str], skipped: List[str], copier=None) -> Dict[str, torch.Tensor]:
+    """One shard's output tensors.  Every target of the file goes to the device, then ONE
+    ``ops.compress_weights`` call quantizes them (same-shape weights in one grouped launch);
+    with ``copier`` the compressed tensors come back through pinned memory asynchronously (valid
+    once the copier's last event completes)."""
     a = sch.weights
     out: Dict[str, torch.Tensor] = {}
+    mods: List[str] = []
+    ws: List[torch.Tensor] = []
     for name in sorted(tensors):
         t = tensors[name]
         if not is_target(name, tuple(t.shape), t.dtype, ignore):
@@ -111,12 +118,24 @@ def _quantize_file(tensors: Dict[str, torch.Tensor], sch: QuantizationScheme, ig
             skipped.append(mod)
             out[name] = t
             continue
-        w = t.to(device, non_blocking=True)
-        comp = ops.compress_weight(w, a, has_activation_quant=sch.input_activations is not None)
-        for k, v in comp.items():
-            out[f"{mod}.{k}"] = v.to("cpu") if v.is_cuda else v
-        quantized.append(mod)
+        mods.append(mod)
+        ws.append(t.to(device, non_blocking=True))
+    if not ws:
+        return out
+    comps = ops.compress_weights(ws, a, has_activation_quant=sch.input_activations is not None)
+    dev_out = {f"{mod}.{k}": v for mod, comp in zip(mods, comps) for k, v in comp.items()}
+    if copier is not None:
+        out.update(copier.submit(dev_out))
+    else:
+        out.update({k: (v.to("cpu") if v.is_cuda else v) for k, v in dev_out.items()})
+    quantized.extend(mods)
     return out
+
+
+def _write_shard(out: Dict[str, torch.Tensor], path: str, ready) -> None:
+    if ready is not None:
+        ready.synchronize()  # the shard's device->host copies have landed
+    save_file({k: v.contiguous() for k, v in out.items()}, path, {"format": "pt"})
 
 
 def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, QuantizationScheme, dict] = "FP8_BLOCK",
@@ -149,20 +168,21 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
     with ThreadPoolExecutor(max_workers=max(2, max_workers)) as pool:
         reads = [pool.submit(_read, os.path.join(model_stub, f)) for f in mine[:2]]
         writes = []
+        copier = _HostCopier(device)
         for i, fn in enumerate(mine):
             tensors = reads[i].result()
             if i + 2 < len(mine):
                 reads.append(pool.submit(_read, os.path.join(model_stub, mine[i + 2])))
-            out = _quantize_file(tensors, sch, ignore, device, quantized, skipped)
-            torch.cuda.current_stream(device).synchronize()
+            out = _quantize_file(tensors, sch, ignore, device, quantized, skipped, copier)
+            ready = copier.last_event
             for k, t in out.items():
                 weight_map[k] = fn
                 total += t.numel() * t.element_size()
-            writes.append(pool.submit(save_file, {k: v.contiguous() for k, v in out.items()},
-                                      os.path.join(save_directory, fn), {"format": "pt"}))
+            writes.append(pool.submit(_write_shard, out, os.path.join(save_directory, fn), ready))
             reads[i] = None
         for w in writes:
             w.result()
+        copier.finish()
     state = (weight_map, total, quantized, skipped)
     if world > 1:
         allst = [None] * world

@@ -169,6 +169,40 @@ def grouped_ok(a: QuantizationArgs, w: torch.Tensor) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
+def _check_no_alias(ws: Sequence[torch.Tensor], outs: Sequence[Dict[str, torch.Tensor]]) -> None:
+    """Raise if any output tensor overlaps any input weight (sorted sweep, O(n log n))."""
+    import bisect
+    ins = sorted((w.data_ptr(), w.data_ptr() + w.numel() * w.element_size()) for w in ws)
+    starts = [lo for lo, _ in ins]
+    run_hi = []  # running max of the end addresses, so one bisect answers "any input overlaps"
+    m = 0
+    for _, hi in ins:
+        m = max(m, hi)
+        run_hi.append(m)
+    for o in outs:
+        for k in ("codes", "scale", "zero_point"):
+            t = o.get(k)
+            if t is None or t.numel() == 0:
+                continue
+            lo, hi = t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()
+            j = bisect.bisect_left(starts, hi) - 1  # inputs starting before this output's end
+            if j >= 0 and run_hi[j] > lo:
+                raise ValueError("GroupedQuantize: an output aliases a weight")
+
+
+def alloc_outputs(shape, a: QuantizationArgs, out_fmt: Optional[int], device) -> Dict[str, torch.Tensor]:
+    """quantize_weight's output tensors for a [rows, cols] or [E, rows, cols] weight."""
+    out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+    lead, (r, c) = tuple(shape[:-2]), tuple(shape[-2:])
+    gshape = n_groups(a, r, c)
+    o = {"codes": _alloc_codes(out_fmt, a, lead, r, c, device),
+         "scale": torch.empty(*lead, *gshape, dtype=_scale_dtype(a), device=device),
+         "zero_point": None if a.symmetric else torch.empty(*lead, *gshape, dtype=torch.int8, device=device)}
+    if a.is_nvfp4:
+        o["global_scale"] = torch.empty(max(int(torch.Size(lead).numel()), 1), dtype=torch.float32, device=device)
+    return o
+
+
 class GroupedQuantize:
     """``qz_quantize_grouped``: n same-shape dense weights quantized in ONE launch (grid.y =
     weight), the per-launch ramp paid once.  The device pointer table is built once here;
@@ -191,23 +225,11 @@ class GroupedQuantize:
         dev = ws[0].device
         self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
         self.ca = a.to_c()
-        gshape = n_groups(a, r, c)
         if outs is None:
-            outs = [{"codes": _alloc_codes(self.out_fmt, a, (), r, c, dev),
-                     "scale": torch.empty(*gshape, dtype=_scale_dtype(a), device=dev),
-                     "zero_point": None if a.symmetric else torch.empty(*gshape, dtype=torch.int8, device=dev)}
-                    for _ in ws]
+            outs = [alloc_outputs((r, c), a, self.out_fmt, dev) for _ in ws]
         if len(outs) != len(ws):
             raise ValueError("GroupedQuantize: one output dict per weight")
-        in_ranges = [(w.data_ptr(), w.data_ptr() + w.numel() * 2) for w in ws]
-        for o in outs:
-            for k in ("codes", "scale", "zero_point"):
-                t = o.get(k)
-                if t is None:
-                    continue
-                lo, hi = t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()
-                if any(lo < b_ and a_ < hi for a_, b_ in in_ranges):
-                    raise ValueError("GroupedQuantize: an output aliases a weight")
+        _check_no_alias(ws, outs)
         if not a.symmetric and any(o.get("zero_point") is None for o in outs):
             raise ValueError("GroupedQuantize: asymmetric schemes need a zero_point output per weight")
         n = len(ws)
@@ -384,16 +406,24 @@ def pack_to_int32(value: torch.Tensor, num_bits: int, packed_dim: int = 1) -> to
     return out
 
 
-def compress_weight(w: torch.Tensor, a: QuantizationArgs, has_activation_quant: bool = False) -> Dict[str, torch.Tensor]:
-    """One module's on-disk tensors (names pinned by scripts/recombine_weights_MiniMax-M2.1.py:54-65):
-    pack-quantized -> weight_packed/weight_scale/weight_shape[/weight_zero_point];
-    float-quantized -> weight/weight_scale; nvfp4/mxfp4-pack-quantized -> weight_packed/weight_scale
-    [/weight_global_scale]."""
+def _compress_plan(a: QuantizationArgs, has_activation_quant: bool) -> Tuple[bool, Optional[int]]:
+    """(int_q, out_fmt) of a module's compressed-tensors format: int8 weights of a W8A8 scheme stay
+    unpacked (``weight``), other int schemes are ``pack-quantized`` (4/8-bit packed by the kernel,
+    other widths quantized to int8 and packed by ``pack_to_int32``); float schemes use the
+    kernel's default output (FP8 bytes / packed FP4)."""
+    if a.type != "int":
+        return False, None
+    int_q = has_activation_quant and a.num_bits == 8
+    fmt = _lib.QZ_OUT_INT8 if (int_q or a.num_bits not in (4, 8)) else _lib.QZ_OUT_PACKED_INT32
+    return int_q, fmt
+
+
+def _compressed_tensors(q: Dict[str, torch.Tensor], w_shape, a: QuantizationArgs, int_q: bool,
+                        fmt: Optional[int]) -> Dict[str, torch.Tensor]:
+    """A quantize_weight result -> the module's on-disk tensors (names pinned by
+    scripts/recombine_weights_MiniMax-M2.1.py:54-65)."""
     out: Dict[str, torch.Tensor] = {}
     if a.type == "int":
-        int_q = has_activation_quant and a.num_bits == 8
-        fmt = _lib.QZ_OUT_INT8 if (int_q or a.num_bits not in (4, 8)) else _lib.QZ_OUT_PACKED_INT32
-        q = quantize_weight(w, a, out_fmt=fmt)
         codes = q["codes"]
         if fmt == _lib.QZ_OUT_INT8 and not int_q:
             codes = pack_to_int32(codes.reshape(-1, codes.shape[-1]), a.num_bits).reshape(
@@ -402,19 +432,17 @@ def compress_weight(w: torch.Tensor, a: QuantizationArgs, has_activation_quant: 
             out["weight"] = codes
         else:
             out["weight_packed"] = codes
-            out["weight_shape"] = torch.tensor(list(w.shape[-2:]))
+            out["weight_shape"] = torch.tensor(list(w_shape[-2:]))
         out["weight_scale"] = q["scale"]
         if not a.symmetric and a.strategy in ("group", "channel"):
             zp = q["zero_point"]
             if int_q:
                 out["weight_zero_point"] = zp
+            elif zp.dim() == 2:
+                out["weight_zero_point"] = pack_to_int32(zp, a.num_bits, packed_dim=0)
             else:
-                if zp.dim() == 2:
-                    out["weight_zero_point"] = pack_to_int32(zp, a.num_bits, packed_dim=0)
-                else:
-                    out["weight_zero_point"] = torch.stack([pack_to_int32(z, a.num_bits, packed_dim=0) for z in zp])
+                out["weight_zero_point"] = torch.stack([pack_to_int32(z, a.num_bits, packed_dim=0) for z in zp])
         return out
-    q = quantize_weight(w, a)
     if a.num_bits == 8:
         out["weight"] = q["codes"]
         out["weight_scale"] = q["scale"]
@@ -423,8 +451,29 @@ def compress_weight(w: torch.Tensor, a: QuantizationArgs, has_activation_quant: 
         out["weight_scale"] = q["scale"]
         if a.is_nvfp4:
             gs = q["global_scale"]
-            out["weight_global_scale"] = gs if w.dim() == 3 else gs.reshape(1)
+            out["weight_global_scale"] = gs if len(w_shape) == 3 else gs.reshape(1)
     return out
+
+
+def compress_weight(w: torch.Tensor, a: QuantizationArgs, has_activation_quant: bool = False) -> Dict[str, torch.Tensor]:
+    """One module's on-disk tensors (names pinned by scripts/recombine_weights_MiniMax-M2.1.py:54-65):
+    pack-quantized -> weight_packed/weight_scale/weight_shape[/weight_zero_point];
+    float-quantized -> weight/weight_scale; nvfp4/mxfp4-pack-quantized -> weight_packed/weight_scale
+    [/weight_global_scale]."""
+    int_q, fmt = _compress_plan(a, has_activation_quant)
+    return _compressed_tensors(quantize_weight(w, a, out_fmt=fmt), tuple(w.shape), a, int_q, fmt)
+
+
+def compress_weights(ws: Sequence[torch.Tensor], a: QuantizationArgs,
+                     has_activation_quant: bool = False) -> List[Dict[str, torch.Tensor]]:
+    """``compress_weight`` over many modules of one scheme -- the compressor's per-module loop
+    (ModelCompressor.compress_model, reached from scripts/do_oneshot.py:197).  Same-shape dense
+    weights under a single-pass group scheme are quantized in ONE grouped launch per shape
+    (qz_quantize_grouped: the ~3 us launch ramp paid once per shape, not once per module); any
+    other weight is one launch.  Results are bit-identical to ``compress_weight`` per module."""
+    int_q, fmt = _compress_plan(a, has_activation_quant)
+    qs = quantize_weights(ws, a, out_fmt=fmt)
+    return [_compressed_tensors(q, tuple(w.shape), a, int_q, fmt) for q, w in zip(qs, ws)]
 
 
 # ------------------------------------------------------------------------------- AWQ

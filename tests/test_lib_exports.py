@@ -26,7 +26,9 @@ def test_library_exports_header_symbols():
 def test_host_only_entry_points():
     from quantizers_amd import _lib
     lib = _lib.load()
-    assert lib.qz_version() == 100
+    assert lib.qz_version() == 200
+    cfg = _lib.build_config()
+    assert cfg["arch"] == "gfx950" and isinstance(cfg["nt_bytes_q"], int)
     assert lib.qz_strerror(-3).decode().startswith("tensor column shape")
     a = _lib.QzArgs(4, 0, 1, 2, 128, 0, 0, 0)
     assert lib.qz_quantize_workspace_size(1, 11008, 4096, ctypes.byref(a)) > 0
