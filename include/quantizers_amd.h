@@ -201,10 +201,13 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
  * qz_awq_weight_mean_accum -- adds sum_r |W[r,c]| / (absmax(group(r,c)) + 1e-6) (bf16
  * elementwise, fp64 sum) into wsum[c] for one balance layer W [rows, cols].  group_size =
  * the layer's quantization group (cols for channel strategy).  Replaces [3P] llmcompressor
- * _compute_layer_means.
+ * _compute_layer_means.  Deterministic: fixed-order two-stage reduction through `workspace`
+ * (qz_awq_weight_mean_workspace_size bytes, 8-B aligned; may be 0 bytes for the generic path).
  */
+size_t qz_awq_weight_mean_workspace_size(int64_t rows, int64_t cols, int32_t group_size);
 int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld,
-                             int32_t group_size, double* wsum, qz_stream_t stream);
+                             int32_t group_size, double* wsum, void* workspace,
+                             size_t workspace_bytes, qz_stream_t stream);
 
 /*
  * qz_awq_sq_err_accum -- the grid search's loss numerator: *out += sum over [rows, cols] of

@@ -25,7 +25,8 @@ QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT, QZ_ERR_WORKSPACE, QZ_ERR_ALIGN = 
 EXPORTS = (
     "qz_strerror", "qz_version", "qz_build_config", "qz_quantize_workspace_size", "qz_quantize", "qz_quantize_qparams",
     "qz_observe_minmax", "qz_calculate_qparams", "qz_dequantize", "qz_pack_int32",
-    "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_accum",
+    "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_workspace_size",
+    "qz_awq_weight_mean_accum",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped",
@@ -71,7 +72,8 @@ def load() -> ctypes.CDLL:
         "qz_pack_int32": ([P, I64, I64, I32, I32, P, P], ctypes.c_int),
         "qz_awq_absmean_workspace_size": ([I64, I64], SZ),
         "qz_awq_absmean_accum": ([P, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
-        "qz_awq_weight_mean_accum": ([P, I64, I64, I64, I32, P, P], ctypes.c_int),
+        "qz_awq_weight_mean_workspace_size": ([I64, I64, I32], SZ),
+        "qz_awq_weight_mean_accum": ([P, I64, I64, I64, I32, P, P, SZ, P], ctypes.c_int),
         "qz_awq_grid_scales": ([P, P, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "qz_awq_fake_quant": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
         "qz_awq_grid_scales_batched": ([P, P, I64, I64, ctypes.c_float, I32, P, P], ctypes.c_int),

@@ -393,27 +393,46 @@ def _all_reduce_sum(t: torch.Tensor) -> None:
         dist.all_reduce(t)
 
 
-def _sharded_search(batch: List[ResolvedMapping], search_chunk, chunk: int = 1) -> List[Any]:
+def _sharded_search(batch: List[ResolvedMapping], search_chunk, chunk: int = 1, n_grid: int = 20) -> List[Any]:
     """Run ``search_chunk`` (a list of mappings -> a list of results) over consecutive chunks of
     a batch of independent mappings; under torch.distributed rank r takes chunks r, r + world,
-    ... and the results (ratio, loss, history, scale vector) are all-gathered, so every rank
-    applies identical smoothing.  Chunk boundaries do not depend on the world size, so the
-    result is bit-identical to one process."""
+    ... and the results are exchanged as ONE device tensor collective: every mapping's (found
+    flag, best ratio, best loss, loss history [n_grid], scale vector) is a row of an f64 matrix
+    [mappings, 3 + n_grid + max cols] that is non-zero on exactly one rank, all-reduced (sum, RCCL
+    on nccl) -- exact, so every rank applies identical smoothing.  Chunk boundaries do not depend
+    on the world size, so the result is bit-identical to one process."""
     import torch.distributed as dist
     chunks = [batch[i:i + chunk] for i in range(0, len(batch), chunk)]
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return [f for c in chunks for f in search_chunk(c)]
     world, rank = dist.get_world_size(), dist.get_rank()
-    mine = {}
-    for j in range(rank, len(chunks), world):
-        mine[j] = [None if f is None else (f[0], f[1], f[2], f[3].cpu()) for f in search_chunk(chunks[j])]
-    gathered: List[Any] = [None] * world
-    dist.all_gather_object(gathered, mine)
     dev = batch[0].balance[0].weight.device
-    per_chunk: Dict[int, List[Any]] = {}
-    for part in gathered:
-        per_chunk.update(part)
-    return [None if f is None else (f[0], f[1], f[2], f[3].to(dev)) for j in range(len(chunks)) for f in per_chunk[j]]
+    cols = [r.balance[0].weight.shape[-1] for r in batch]
+    width = 3 + n_grid + max(cols)
+    table = torch.zeros(len(batch), width, dtype=torch.float64, device=dev)
+    for j in range(rank, len(chunks), world):
+        for k, f in enumerate(search_chunk(chunks[j])):
+            if f is None:
+                continue
+            m = j * chunk + k
+            ratio, best, history, scales = f
+            row = table[m]
+            row[0] = 1.0
+            row[1] = ratio
+            row[2] = best
+            row[3:3 + n_grid] = torch.tensor(history, dtype=torch.float64, device=dev)
+            row[3 + n_grid:3 + n_grid + scales.numel()] = scales.to(torch.float64)
+    _all_reduce_sum(table)
+    out: List[Any] = []
+    for m, r in enumerate(batch):
+        row = table[m]
+        if row[0].item() == 0.0:
+            out.append(None)
+            continue
+        head = row[:3 + n_grid].cpu().tolist()
+        out.append((head[1], head[2], head[3:3 + n_grid],
+                    row[3 + n_grid:3 + n_grid + cols[m]].to(torch.float32).contiguous()))
+    return out
 
 
 def _expert_batchable(batch: List[ResolvedMapping], quantized: Dict[str, QuantizationArgs], calibrate_all: bool) -> bool:
@@ -628,9 +647,9 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             ei = experts[id(b0.module)]
             n_tok = sum(x.shape[0] for x in ei.x)
             w2 = getattr(b0.module, b0.param_name)
-            found = _sharded_search(batch, search_experts, _expert_chunk(n_tok, w2.shape[2], w2.shape[1]))
+            found = _sharded_search(batch, search_experts, _expert_chunk(n_tok, w2.shape[2], w2.shape[1]), n_grid)
         else:
-            found = _sharded_search(batch, lambda c: [search(c[0])])
+            found = _sharded_search(batch, lambda c: [search(c[0])], 1, n_grid)
         for r, f in zip(batch, found):
             apply(r, f)
     return report

@@ -83,11 +83,12 @@ __global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, i
 // unrolled so a lane has its chunks in flight together: the stage is latency-bound, ~nch*C*4 B),
 // the FW wave sums are added in a fixed order; accumulated into sum[c]
 constexpr int FW = 16;
-__global__ __launch_bounds__(FW * 64) void k_absmean_final(const float* part, int64_t nch, int64_t C, float* sum) {
-  __shared__ float red[FW][64];
+template <typename T>
+__global__ __launch_bounds__(FW * 64) void k_colsum_final(const T* part, int64_t nch, int64_t C, T* sum) {
+  __shared__ T red[FW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
-  float acc = 0.f;
+  T acc = 0;
   if (c < C) {
 #pragma unroll 8
     for (int64_t k = wv; k < nch; k += FW) acc += part[k * C + c];
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(FW * 64) void k_absmean_final(const float* part, in
   red[wv][lane] = acc;
   __syncthreads();
   if (wv == 0 && c < C) {
-    float t = red[0][lane];
+    T t = red[0][lane];
 #pragma unroll
     for (int w = 1; w < FW; ++w) t += red[w][lane];
     sum[c] += t;
@@ -176,11 +177,21 @@ int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
   return cdiv(T, *tc);
 }
 
+// row chunks of the w_mean stage 1: >= 16 rows each (4 per wave), about 1024 workgroups
+int64_t wmean_chunks(int64_t R, int64_t C, int64_t* rc) {
+  const int64_t bx = cdiv(C, 512);
+  const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, 16), cdiv(1024, bx)));
+  *rc = cdiv(R, nrc);
+  return cdiv(R, *rc);
+}
+
 // ------------------------------------------------- a4: w_mean numerator (f64 sums)
-// block = 4 waves over one 512-column window x a chunk of rows; lane owns 8 columns.
+// stage 1: block = 4 waves over one 512-column window x a chunk of rows; lane owns 8 columns;
+// the 4 wave sums are added in a fixed order -> part[row chunk][c].  Stage 2 (k_colsum_final)
+// adds the chunks in a fixed order: deterministic, like the activation means.
 template <int LOGL>
 __global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t rc,
-                                                  double* wsum) {
+                                                  double* part) {
   constexpr int L = 1 << LOGL;
   __shared__ double red[4][512];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -215,13 +226,11 @@ __global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, 
   __syncthreads();
   for (int j = threadIdx.x; j < 512; j += 256) {
     const int64_t c = (int64_t)blockIdx.x * 512 + j;
-    if (c < C) {
-      const double s = red[0][j] + red[1][j] + red[2][j] + red[3][j];
-      atomicAdd(&wsum[c], s);
-    }
+    if (c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
   }
 }
-// generic: thread per (row, group) element run; any group size / alignment
+// generic: one thread per column walks every row in order (deterministic); any group size /
+// alignment
 __global__ void k_wmean_generic(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t g, double* wsum) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -233,7 +242,7 @@ __global__ void k_wmean_generic(const uint16_t* w, int64_t R, int64_t C, int64_t
     const float d = bfr(m + 1e-6f);
     acc += (double)bfr(fabsf(bf2f(w[r * ld + c])) / d);
   }
-  atomicAdd(&wsum[c], acc);
+  wsum[c] += acc;
 }
 
 // ------------------------------------------------------- a5: one grid point's scales
@@ -353,7 +362,8 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   }
   int rc = launch_err();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_absmean_final, dim3((unsigned)cdiv(channels, 64)), dim3(FW * 64), 0, st, part, nch, channels, sum);
+  hipLaunchKernelGGL(k_colsum_final<float>, dim3((unsigned)cdiv(channels, 64)), dim3(FW * 64), 0, st, part, nch, channels,
+                     sum);
   return launch_err();
 }
 
@@ -379,8 +389,14 @@ int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols
   return launch_err();
 }
 
+size_t qz_awq_weight_mean_workspace_size(int64_t rows, int64_t cols, int32_t group_size) {
+  if (rows <= 0 || cols <= 0 || group_size <= 0) return 0;
+  int64_t rc;
+  return (size_t)8 * (size_t)(wmean_chunks(rows, cols, &rc) * cols);
+}
+
 int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld, int32_t group_size, double* wsum,
-                             qz_stream_t stream) {
+                             void* workspace, size_t workspace_bytes, qz_stream_t stream) {
   if (!w || !wsum) return QZ_ERR_NULL;
   if (rows <= 0 || cols <= 0 || ld < cols) return QZ_ERR_SHAPE;
   if (group_size <= 0 || cols % group_size) return QZ_ERR_GROUP;
@@ -388,22 +404,29 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
   const int64_t g = group_size;
   const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
   if (pow2 && ld % 8 == 0 && aligned(w, 16)) {
-    const int64_t bx = cdiv(cols, 512);
-    const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(rows, 16), cdiv(1024, bx)));
-    const int64_t rc = cdiv(rows, nrc);
-    dim3 grid((unsigned)bx, (unsigned)cdiv(rows, rc));
+    if (!workspace || workspace_bytes < qz_awq_weight_mean_workspace_size(rows, cols, group_size))
+      return QZ_ERR_WORKSPACE;
+    if (!aligned(workspace, 8)) return QZ_ERR_ALIGN;
+    int64_t rc;
+    const int64_t nch = wmean_chunks(rows, cols, &rc);
+    dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nch);
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const uint16_t* wp = (const uint16_t*)w;
+    double* part = (double*)workspace;
     switch (logl) {
-      case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      case 1: hipLaunchKernelGGL(k_wmean_v8<1>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      case 2: hipLaunchKernelGGL(k_wmean_v8<2>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      case 3: hipLaunchKernelGGL(k_wmean_v8<3>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      case 4: hipLaunchKernelGGL(k_wmean_v8<4>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      case 5: hipLaunchKernelGGL(k_wmean_v8<5>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
-      default: hipLaunchKernelGGL(k_wmean_v8<6>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, wsum); break;
+      case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 1: hipLaunchKernelGGL(k_wmean_v8<1>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 2: hipLaunchKernelGGL(k_wmean_v8<2>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 3: hipLaunchKernelGGL(k_wmean_v8<3>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 4: hipLaunchKernelGGL(k_wmean_v8<4>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 5: hipLaunchKernelGGL(k_wmean_v8<5>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      default: hipLaunchKernelGGL(k_wmean_v8<6>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
     }
+    int e = launch_err();
+    if (e) return e;
+    hipLaunchKernelGGL(k_colsum_final<double>, dim3((unsigned)cdiv(cols, 64)), dim3(FW * 64), 0, st, part, nch, cols,
+                       wsum);
   } else {
     hipLaunchKernelGGL(k_wmean_generic, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const uint16_t*)w, rows,
                        cols, ld, g, wsum);

@@ -494,13 +494,17 @@ def awq_absmean_accum(x: torch.Tensor, sums: torch.Tensor) -> int:
 
 
 def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) -> int:
-    """wsum[c] += sum_r |W[r,c]| / (group absmax + 1e-6) (fp64).  Returns rows added."""
+    """wsum[c] += sum_r |W[r,c]| / (group absmax + 1e-6) (fp64, deterministic: fixed-order
+    two-stage reduction).  Returns rows added."""
     _check_dev(w, "weight")
     w2 = w.reshape(-1, w.shape[-1])
     if w2.stride(-1) != 1:
         w2 = w2.contiguous()
     r, c = w2.shape
-    rc = _lib.load().qz_awq_weight_mean_accum(_ptr(w2), r, c, w2.stride(0), int(group_size), _ptr(wsum), _stream())
+    lib = _lib.load()
+    ws = workspace(lib.qz_awq_weight_mean_workspace_size(r, c, int(group_size)) + 256, w.device)
+    rc = lib.qz_awq_weight_mean_accum(_ptr(w2), r, c, w2.stride(0), int(group_size), _ptr(wsum), _ptr(ws), ws.numel(),
+                                      _stream())
     _lib.check(rc, "qz_awq_weight_mean_accum")
     return r
 

@@ -16,10 +16,10 @@ step() {  # step <name> <timeout> <cmd...>
   if [ $rc -ne 0 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
-[ "${SKIP_BENCH:-0}" = 1 ] || step bench 600 python bench.py ${BENCH_ARGS:-}
+[ "${SKIP_TESTS:-0}" = 1 ] || step pytest_gpu 420 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}
+[ "${SKIP_BENCH:-0}" = 1 ] || step bench 300 python bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = 1 ]; then
-  step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_${TAG}" -o run -- \
+  step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_${TAG}" -o run -- \
        python3 "$PWD/bench.py" ${BENCH_ARGS:-}
 fi
 echo "=== done"

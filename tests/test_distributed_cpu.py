@@ -89,3 +89,120 @@ def test_sharded_compress_gloo_world2():
 def test_gather_single_process_passthrough():
     t = {"x": torch.arange(5)}
     assert gather_state(t) == t
+
+
+# ---------------------------------------------------------------- save_compressed, 2 ranks
+class _OraclePlan:
+    """Stand-in for compressor.CompressionPlan on a CPU-only host (test infrastructure): the
+    units are compressed by the CPU oracle, so the sharding / gather / rank-0 write logic of
+    save_compressed runs here; on GPUs the same logic drives the HIP kernels (tests/
+    test_multirank_save_gpu.py)."""
+
+    def __init__(self, units, device):
+        import ct_torch as ct
+        self.out = {}
+        for u in units:
+            a = u.scheme.weights
+            oa = ct.QArgs(num_bits=a.num_bits, type=a.type, symmetric=a.symmetric, strategy=a.strategy,
+                          group_size=a.group_size)
+            for ref in u.refs:
+                for k, v in ct.compress_weight(ref.weight.detach().contiguous(), oa).items():
+                    self.out[f"{ref.name}.{k}"] = v
+
+    def run(self, stream=None):
+        pass
+
+    def tensors(self):
+        return dict(self.out)
+
+
+def _tiny_model():
+    from torch import nn
+    from quantizers_amd.quantization import QuantizationArgs, QuantizationScheme
+    torch.manual_seed(0)
+    m = nn.Module()
+    m.model = nn.Module()
+    m.model.layers = nn.ModuleList()
+    for _ in range(3):
+        blk = nn.Module()
+        blk.q_proj = nn.Linear(64, 96, bias=False)
+        blk.up_proj = nn.Linear(64, 128, bias=True)
+        blk.norm = nn.LayerNorm(64)
+        m.model.layers.append(blk)
+    m.lm_head = nn.Linear(64, 32, bias=False)
+    m.to(torch.bfloat16)
+    sch = QuantizationScheme(targets=["Linear"], weights=QuantizationArgs(num_bits=4, type="int", symmetric=True,
+                                                                          group_size=32))
+    m.quantization_scheme_map = {f"model.layers.{i}.{p}": sch for i in range(3) for p in ("q_proj", "up_proj")}
+    return m
+
+
+def _save_worker(rank, world, port, out_dir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+        from quantizers_amd import compressor
+        compressor.CompressionPlan = _OraclePlan
+        compressor.save_compressed(_tiny_model(), out_dir, device="cpu")
+        q.put((rank, sorted(os.listdir(out_dir))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_save_compressed_gloo_world2_matches_one_process(tmp_path):
+    import filecmp
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
+    from quantizers_amd import compressor
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    multi = str(tmp_path / "multi")
+    procs = [ctx.Process(target=_save_worker, args=(r, 2, port, multi, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][1] == res[1][1] and "model.safetensors" in res[0][1]
+    saved = compressor.CompressionPlan
+    compressor.CompressionPlan = _OraclePlan
+    try:
+        one = compressor.save_compressed(_tiny_model(), str(tmp_path / "one"), device="cpu")
+    finally:
+        compressor.CompressionPlan = saved
+    for fn in ("model.safetensors", "config.json"):
+        assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        local = {f"r{rank}.t{i}": torch.arange(i * 7 + rank * 3 + 1, dtype=torch.int16) for i in range(5)}
+        local[f"r{rank}.e"] = torch.empty(0, dtype=torch.float32)
+        # tiny buckets: several all-gather rounds, ragged per-rank sizes
+        out = gather_state(local, dst=1, to_host=True, bucket_bytes=64)
+        q.put((rank, {k: v.tolist() for k, v in out.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_state_buckets_and_dst():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == {} and res[2] == {}
+    want = {f"r{r}.t{i}": list(range(i * 7 + r * 3 + 1)) for r in range(3) for i in range(5)}
+    want.update({f"r{r}.e": [] for r in range(3)})
+    assert res[1] == want

@@ -1,0 +1,57 @@
+"""Multi-rank product path on one card: ``oneshot`` (AWQ) + ``save_compressed`` under
+torch.distributed (2 ranks, gloo control plane sharing cuda:0) -- compression sharded over the
+ranks by ``plan_shards``, reassembled by ``gather_state``, written by rank 0 -- produces a
+checkpoint byte-identical to the one-process run."""
+import filecmp
+import os
+import socket
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RECIPE = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g32.yaml")
+
+
+def _model_and_data():
+    from test_oneshot_gpu import _calib, _qwen3
+    return _qwen3(layers=2), _calib()
+
+
+def _rank(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizers_amd.compressor import save_compressed
+        from quantizers_amd.oneshot import oneshot
+        m, data = _model_and_data()
+        m = m.to("cuda:0")
+        oneshot(m, RECIPE, dataset=data, max_seq_length=64)
+        save_compressed(m, out_dir)
+    finally:
+        dist.destroy_process_group()
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_save_compressed_two_ranks_byte_identical(cuda, tmp_path):
+    import torch.multiprocessing as mp
+    from quantizers_amd.compressor import save_compressed
+    from quantizers_amd.oneshot import oneshot
+    multi = str(tmp_path / "two_ranks")
+    mp.spawn(_rank, args=(2, _port(), multi), nprocs=2, join=True)
+    m, data = _model_and_data()
+    m = m.to(cuda)
+    oneshot(m, RECIPE, dataset=data, max_seq_length=64)
+    one = save_compressed(m, str(tmp_path / "one_process"))
+    for fn in ("model.safetensors", "config.json", "recipe.yaml"):
+        assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn

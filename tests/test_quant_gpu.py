@@ -238,6 +238,65 @@ def test_awq_stats(cuda):
         torch.testing.assert_close(got.cpu(), ct.awq_grid_scales(xm, ref, ratio, True), rtol=2e-6, atol=1e-7)
 
 
+def _wmean_tree(w: torch.Tensor, g: int) -> torch.Tensor:
+    """Fixed-order restatement of qz_awq_weight_mean_accum's reduction tree (one call into a
+    zero wsum): terms bf16(|w| / bf16(group absmax + 1e-6)) (the oracle's elementwise values),
+    summed in f64 exactly as the two kernels do -- per row chunk, wave j sums rows j, j+4, ... in
+    order, chunk = ((s0 + s1) + s2) + s3; then wave v of stage 2 sums chunks v, v+16, ... and the
+    16 wave sums are added in order."""
+    import numpy as np
+    R, C = w.shape
+    v = w.reshape(-1, g).abs()
+    v = (v / (v.amax(dim=1, keepdim=True) + 1e-6)).reshape(R, C).double().numpy()
+    bx = -(-C // 512)
+    nrc = max(1, min(-(-R // 16), -(-1024 // bx)))
+    rc = -(-R // nrc)
+    nch = -(-R // rc)
+    part = np.zeros((nch, C))
+    for k in range(nch):
+        r0, r1 = k * rc, min(R, (k + 1) * rc)
+        ws = []
+        for j in range(4):
+            acc = np.zeros(C)
+            for r in range(r0 + j, r1, 4):
+                acc = acc + v[r]
+            ws.append(acc)
+        part[k] = ((ws[0] + ws[1]) + ws[2]) + ws[3]
+    red = []
+    for wv in range(16):
+        acc = np.zeros(C)
+        for k in range(wv, nch, 16):
+            acc = acc + part[k]
+        red.append(acc)
+    t = red[0]
+    for wv in range(1, 16):
+        t = t + red[wv]
+    return torch.from_numpy(np.zeros(C) + t)
+
+
+@pytest.mark.parametrize("shape,g", [((320, 512), 32), ((2000, 1536), 128), ((37, 4096), 64)])
+def test_weight_mean_deterministic_fixed_order(cuda, shape, g):
+    """w_mean is a fixed-order two-stage reduction: bit-identical to the restated tree, and
+    identical across repeated calls while other work runs concurrently on another stream."""
+    w = _w(*shape, seed=11)
+    wc = w.to(cuda)
+    want = _wmean_tree(w, g)
+    outs = []
+    side = torch.cuda.Stream()
+    junk = torch.randn(4096, 4096, device=cuda)
+    for i in range(4):
+        wsum = torch.zeros(shape[1], dtype=torch.float64, device=cuda)
+        if i % 2:
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    junk = junk @ junk.T / 4096  # concurrent load on the card
+        ops.awq_weight_mean_accum(wc, g, wsum)
+        torch.cuda.synchronize()
+        outs.append(wsum.cpu())
+    for o in outs:
+        assert torch.equal(o, want), (o - want).abs().max()
+
+
 def test_smoothing_ops(cuda):
     w = _w(64, 128, seed=2)
     s = torch.rand(128, generator=torch.Generator().manual_seed(1)) + 0.5
