@@ -2,10 +2,16 @@
 same output-directory rule) on the MI355X path.
 
 Reference flags (scripts/do_oneshot.py:47-79): --config, --output, --cache-dir, --log-file,
---debug.  Offline additions (no Hub access in this environment): --model-path (a local HF model
-directory instead of ``model.name``), --random-init (build ``model.name``'s architecture from a
-local config with random weights), --calib-file (tokenized calibration set: .pt tensor
-[N, S] or .jsonl rows with ``input_ids``) and --calib-random N,S (synthetic token ids).
+--debug.  Calibration data as in the reference (do_oneshot.py:137-169): the run config's
+``calibration_set`` is looked up in ``--cache-dir`` under the reference's cache key and
+tokenized with the model's tokenizer (``calibration.py``); the tokenizer is saved next to the
+checkpoint (do_oneshot.py:198).  Offline additions (no Hub access in this environment):
+--model-path (a local HF model directory instead of ``model.name``), --random-init (build
+``model.name``'s architecture from a local config with random weights), --tokenizer (a local
+tokenizer directory when the model has none), --calib-file (tokenized calibration set: .pt
+tensor [N, S] or .jsonl rows with ``input_ids``) and --calib-random N,S (synthetic token ids).
+Under torchrun every rank runs the calibration (AWQ grid ratios / expert searches split over the
+ranks) and the compression is sharded; rank 0 alone writes the output directory.
 """
 from __future__ import annotations
 
@@ -38,6 +44,7 @@ def parse_args(argv=None):
     p.add_argument("--model-path", type=str, default=None, help="local model directory (offline)")
     p.add_argument("--random-init", type=str, default=None,
                    help="HF config.json (file or dir) to build a random-weight model from")
+    p.add_argument("--tokenizer", type=str, default=None, help="local tokenizer directory (offline)")
     p.add_argument("--calib-file", type=str, default=None)
     p.add_argument("--calib-random", type=str, default=None, help="N,S synthetic calibration tokens")
     p.add_argument("--max-seq-length", type=int, default=None)
@@ -45,7 +52,9 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
-def _calibration(args, run, vocab: int):
+def _calibration(args, run, vocab: int, tokenizer=None):
+    """Tokenized calibration rows: --calib-file / --calib-random, else the run config's
+    calibration set read from the reference-format cache in --cache-dir (do_oneshot.py:143-169)."""
     if args.calib_file:
         if args.calib_file.endswith(".pt"):
             t = torch.load(args.calib_file, weights_only=True)
@@ -59,6 +68,29 @@ def _calibration(args, run, vocab: int):
         n, s = (int(x) for x in args.calib_random.split(","))
         g = torch.Generator().manual_seed(42)  # reference shuffle seed (calibration_sets.py:618-619)
         return [{"input_ids": torch.randint(0, vocab, (s,), generator=g)} for _ in range(n)]
+    if run.calibration:
+        from . import calibration
+        if tokenizer is None:
+            raise ValueError("the calibration set needs the model's tokenizer: pass --model-path (a local model "
+                             "directory with a tokenizer) or --tokenizer")
+        t0 = time.time()
+        rows = calibration.load_tokenized(run.calibration, args.cache_dir, tokenizer)
+        logging.info("Loaded calibration set from cache %s (%d samples) in %.2f seconds",
+                     calibration.cache_path(run.calibration, args.cache_dir), len(rows), time.time() - t0)
+        return rows
+    return None
+
+
+def load_tokenizer(args, run):
+    """The model's tokenizer (do_oneshot.py:94) from a local directory: --tokenizer, else
+    --model-path, else ``model.name`` when it is a local directory; None when there is none."""
+    from transformers import AutoTokenizer
+    for path in (args.tokenizer, args.model_path, run.model.name):
+        if path and os.path.isdir(path):
+            try:
+                return AutoTokenizer.from_pretrained(path)
+            except (OSError, ValueError) as e:
+                logging.debug("no tokenizer in %s: %s", path, e)
     return None
 
 
@@ -73,6 +105,11 @@ def load_model(args, run):
                                                 trust_remote_code=True)
 
 
+def _rank() -> int:
+    import torch.distributed as dist
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 def main(argv=None):
     args = parse_args(argv)
     setup_logging(args.log_file, logging.DEBUG if args.debug else logging.INFO)
@@ -85,8 +122,9 @@ def main(argv=None):
     output_dir = args.output or run.output_dir()
     recipe_path = run.resolve_recipe()
     model = load_model(args, run)
+    tokenizer = load_tokenizer(args, run)
     vocab = getattr(model.config, "vocab_size", 32000)
-    dataset = _calibration(args, run, vocab)
+    dataset = _calibration(args, run, vocab, tokenizer)
     max_len = args.max_seq_length or (run.calibration or {}).get("max_seq_length", 2048)
     logging.info("Starting quantization")
     t0 = time.time()
@@ -94,10 +132,13 @@ def main(argv=None):
             num_calibration_samples=len(dataset) if dataset else None, moe_calibrate_all_experts=True,
             device=args.device)
     logging.info("Completed quantization in %.2f seconds", time.time() - t0)
-    os.makedirs("outputs", exist_ok=True)
+    if _rank() == 0:
+        os.makedirs("outputs", exist_ok=True)
     logging.info("Saving quantized model to: %s", output_dir)
     t0 = time.time()
-    save_compressed(model, output_dir)
+    save_compressed(model, output_dir)  # sharded over ranks under torchrun; rank 0 writes
+    if tokenizer is not None and _rank() == 0:
+        tokenizer.save_pretrained(output_dir)
     logging.info("Saved quantized model in %.2f seconds", time.time() - t0)
     logging.info("SUCCESS: Quantized model saved in %s", output_dir)
     return output_dir

@@ -1,13 +1,16 @@
 """Run configuration: the reference's 3-level YAML (run config -> recipe path + calibration set),
 same keys and path resolution as src/quantizers/config.py:52-114 and scripts/do_oneshot.py:111-135.
-The calibration-set *content* pipeline (HF datasets, formatters, parquet cache;
-src/quantizers/calibration_sets.py) is network-bound host plumbing and out of scope: a
-calibration set is read from a local tokenized file or synthesised (see cli.py)."""
+The calibration-set file is parsed and validated as the reference does
+(CalibrationSetConfig.from_file, src/quantizers/calibration_sets.py:208-247); its *content*
+comes from the reference-format parquet cache (calibration.py) -- building it from Hub datasets
+is network-bound and out of scope -- or from a local tokenized file / synthetic ids (cli.py)."""
 from __future__ import annotations
 
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Any, Dict, Optional
+
+import logging
 
 import yaml
 
@@ -63,7 +66,10 @@ def load_run_config(path: str) -> RunConfig:
             base = p.parent
             cp = str(base / cp[len("configs/"):]) if cp.startswith("configs/") else str(base / cp)
         if Path(cp).exists():
-            calib_cfg = yaml.safe_load(Path(cp).read_text())
+            from .calibration import normalise
+            calib_cfg = normalise(yaml.safe_load(Path(cp).read_text()) or {})
+        else:  # the reference raises here; offline runs may still pass --calib-file / --calib-random
+            logging.getLogger(__name__).warning("Calibration set not found: %s", cp)
         calib = cp
     return RunConfig(model=ModelConfig(m["name"], m.get("revision", "main")), recipe=q["recipe"],
                      calibration_set=calib, calibration=calib_cfg, config_path=str(p))

@@ -10,9 +10,10 @@ command's stdout (its JSON line).  Writes
   profiles/TAG_kernel_stats.csv   -- the stats table (torch generator names shortened)
   profiles/TAG_bench_line.json    -- the bench line of the same run
   profiles/TAG_headline.json      -- the headline launches picked from the trace: the grouped
-      kernel's dispatches with grid.y = 36 (one per Qwen3-4B shape class) in dispatch order:
+      kernel's dispatches in dispatch order:
       W*L warmup, then the K*L timed launches (L = launches per step), then L per-launch probes;
-      their mean duration, kernel time per step, and frac = alg bytes per step / kernel time per
+      their mean duration (the headline launches are told apart from the synthetic leg's by their
+      grid.y = weights per launch, e.g. 36 / 72 for Qwen3-4B; the synthetic leg uses 100), kernel time per step, and frac = alg bytes per step / kernel time per
       step / 8 TB/s next to the line's own frac.
 """
 import csv
@@ -58,7 +59,8 @@ def main(tag, prof_dir, bench_log):
     kern = line["roofline"]["kernel"]
     L = int(line["roofline"]["launches_per_step"])
     K, W = int(line["steps"]), int(line["warmup"])
-    mine = [r for r in trace if kern in r["Kernel_Name"] and int(r.get("Grid_Size_Y", r.get("Grid_Size_y", 0))) == 36]
+    gy = {int(p["weights"]) for p in line["per_launch"]}  # grid.y of the headline launches (weights each)
+    mine = [r for r in trace if kern in r["Kernel_Name"] and int(r.get("Grid_Size_Y", r.get("Grid_Size_y", 0))) in gy]
     mine.sort(key=lambda r: int(r["Start_Timestamp"]))
     timed = mine[W * L:(W + K) * L]
     if len(timed) != K * L:
