@@ -185,12 +185,13 @@ struct GP {
 
 // calculate_qparams for one group from its observed min/max (bf16 values as f32).
 // gs: NVFP4 global scale (K_NV only).
-__device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, float gs) {
+// mx_is_absmax: symmetric group whose caller passes max(|min|, |max|) as mx (mn unused)
+__device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, float gs, bool mx_is_absmax = false) {
   GP g;
   float lo = fminf(mn, 0.f), hi = fmaxf(mx, 0.f);
   g.zp = 0.f;
   if (p.kind == K_MX) {
-    float am = fmaxf(fabsf(lo), fabsf(hi));
+    float am = mx_is_absmax ? mx : fmaxf(fabsf(lo), fabsf(hi));
     uint32_t b = f2bf(am);
     uint32_t e = ((b + 0x40u) >> 7) & 0xffu;  // round_to_power_2 -> exponent field
     int byte = (int)e - 2;
@@ -204,7 +205,7 @@ __device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, floa
   }
   float s;
   if (p.sym) {
-    float am = fmaxf(fabsf(lo), fabsf(hi));
+    float am = mx_is_absmax ? mx : fmaxf(fabsf(lo), fabsf(hi));
     s = (am == 0.f) ? 0.f : bf16_quot(am, p.half_range, p.inv_half);
   } else {
     const float rng = bfr(hi - lo);

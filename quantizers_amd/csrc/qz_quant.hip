@@ -520,6 +520,178 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
   process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES, UNROLL>(A, p, v, b, tile, lane, csu);
 }
 
+// ------------------------------------------------ AWQ fake-quant with column scales
+// Q(W*s)/s of the AWQ grid (qz_awq_fake_quant[_batched]; group strategy, power-of-two groups of
+// 8..512, dense rows).  A wave's tile is FQ_ROWS rows x 64 lanes, and every lane owns the SAME 8
+// columns in each of those rows, so the column scales, their reciprocals and the range check
+// are fetched / computed once per tile instead of once per 8 elements.  The unit-wise
+// k_group_fast<..., FQ=true> issued 457 VALU instructions per wave (2 units per lane) and was
+// VALU-bound (PMC r02c: 41.9 us for [11008, 4096], 0.54 of 8 TB/s).  grid = (column chunks of
+// 64 units, row blocks / waves per workgroup, batch): consecutive workgroups cover one row
+// block's chunks, so the stream stays contiguous.
+#ifndef QZ_FQ_ROWS
+#define QZ_FQ_ROWS 4
+#endif
+constexpr int FQ_ROWS = QZ_FQ_ROWS;
+
+// bf16(d / c) for a pair given r = rcp(c), packed: the IEEE division only when a quotient lies
+// within 4 ulps of a bf16 rounding midpoint (low 16 bits near 0x8000; 16-bit adds) or when
+// the lane's column scales are outside the range where rcp is accurate (ok == false)
+// near-midpoint test of a quotient pair: the two low halves packed (v_perm), +0x8004 on both
+// (v_pk_add_u16), then the smaller half below 8 means one of them is within 4 ulps of 0x8000
+__device__ __forceinline__ bool near_mid_pk(const f32x2 q) {
+  const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(q.y), __float_as_uint(q.x), 0x05040100u);
+  const u16x2 a = __builtin_bit_cast(u16x2, lo) + (u16x2){0x8004, 0x8004};
+  return min(a.x, a.y) < 8;
+}
+
+// widen a packed bf16 pair to f32
+__device__ __forceinline__ f32x2 unpk(const uint32_t u) {
+  return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+
+// one unit (8 elements of one row, one lane): W' = bf16(W * s) -> observe the group of W' ->
+// qparams -> quantize -> dequantize -> bf16(fl32(dq / s)); the same op sequence as
+// encode_store<KIND, FQ=true> (compressed-tensors' fake_quantize on the scaled weight, then the
+// f32 division by the column scales)
+template <int LOGL, int KIND, bool SYM>
+__device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2* cs, const f32x2* rc, const bool cs_ok) {
+  constexpr int L = 1 << LOGL;
+  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+  uint32_t xw[4];
+  f32x2 x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    xw[k] = pk_bf16(unpk(wd[k]) * cs[k]);  // W * s in the weight dtype
+    x[k] = unpk(xw[k]);
+  }
+  float mn, mx;
+  if (SYM) {  // |bf16| bit patterns, two per dword
+    const uint32_t m = pk_max_u16(pk_max_u16(xw[0] & 0x7fff7fffu, xw[1] & 0x7fff7fffu),
+                                  pk_max_u16(xw[2] & 0x7fff7fffu, xw[3] & 0x7fff7fffu));
+    const uint32_t am = grp_max_u<L>(max(m & 0xffffu, m >> 16) << 16);
+    mx = __uint_as_float(am);
+    mn = -mx;
+  } else {
+    uint32_t kmn = 0xffffffffu, kmx = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t a = f2key(x[k].x), b = f2key(x[k].y);
+      kmn = min(kmn, min(a, b));
+      kmx = max(kmx, max(a, b));
+    }
+    mn = key2f(grp_min_u<L>(kmn));
+    mx = key2f(grp_max_u<L>(kmx));
+  }
+  QP ps = p;
+  ps.sym = SYM;
+  ps.kind = KIND;
+  const GP g = group_params(ps, mn, mx, 0.f, SYM);
+  // quotient x / scale in bf16 (x * rcp(s): rcp lemma)
+  f32x2 t[4];
+  const f32x2 rs2 = {g.rs, g.rs};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = x[k] * rs2;
+  if (__builtin_expect(!g.fast, 0)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { t[k].x = x[k].x / g.s; t[k].y = x[k].y / g.s; }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) t[k] = unpk(pk_bf16(t[k]));
+  const f32x2 s2 = {g.s, g.s};
+  f32x2 dq[4];
+  if (KIND == K_INT) {
+    const f32x2 zp2 = {g.zp, g.zp};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f32x2 tk = t[k];
+      if (!SYM) tk = unpk(pk_bf16(tk + zp2));
+      const f32x2 r = {__builtin_rintf(__builtin_amdgcn_fmed3f(tk.x, p.qmin, p.qmax)),
+                       __builtin_rintf(__builtin_amdgcn_fmed3f(tk.y, p.qmin, p.qmax))};
+      // symmetric: the zero point is 0 and r - 0 == r exactly (sign of zero kept)
+      dq[k] = SYM ? unpk(pk_bf16(r * s2)) : unpk(pk_bf16(unpk(pk_bf16(r - zp2)) * s2));
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      uint32_t c0, c1;
+      if (KIND == K_FP8) {
+        const uint32_t pk = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f),
+                                                                      __builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f), 0, false);
+        c0 = pk & 0xffu;
+        c1 = (pk >> 8) & 0xffu;
+      } else {  // MXFP4 / FP4 (E2M1 RNE, as encode_store)
+        const uint32_t pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(
+            0u, __builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f) + 0.0f, __builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f) + 0.0f,
+            1.0f, 0);
+        c0 = pk & 0xfu;
+        c1 = (pk >> 4) & 0xfu;
+      }
+      dq[k] = f32x2{decode(ps, g, c0), decode(ps, g, c1)};
+    }
+  }
+  // ÷ column scale: bf16(d * rcp(c)) unless a quotient is within 4 ulps of a bf16 rounding
+  // midpoint or a scale is outside rcp's accurate range -- then the IEEE division (one branch
+  // per unit; taken by ~6 % of the waves' units on Gaussian weights)
+  f32x2 q[4];
+  bool near = !cs_ok;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    q[k] = dq[k] * rc[k];
+    near |= near_mid_pk(q[k]);
+  }
+  if (__builtin_expect(near, 0)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q[k] = f32x2{dq[k].x / cs[k].x, dq[k].y / cs[k].y};
+  }
+  return make_uint4(pk_bf16(q[0]), pk_bf16(q[1]), pk_bf16(q[2]), pk_bf16(q[3]));
+}
+
+template <int LOGL, int KIND, bool SYM, bool NT>
+__global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
+  constexpr int U = FQ_ROWS;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + (threadIdx.x >> 6);
+  if (rblk * U >= rows) return;
+  const int64_t b = blockIdx.z;
+  const int64_t upr = A.units_per_row;
+  const int64_t cu = (int64_t)blockIdx.x * WAVE + lane;  // this lane's column unit
+  const bool col_ok = cu < upr;
+  const int64_t cuc = col_ok ? cu : upr - 1;
+  const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
+  uint4 v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    int64_t r = rblk * U + u;
+    r = r < rows ? r : rows - 1;
+    const uint4* ptr = src + r * upr + cuc;
+    if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr)));
+    else v[u] = *ptr;
+  }
+  // this lane's 8 column scales, their reciprocals, and whether rcp is accurate for all 8
+  const float* csp = A.col_scales + b * A.cs_ld_batch + cuc * 8;
+  const float4 c_lo = *reinterpret_cast<const float4*>(csp);
+  const float4 c_hi = *reinterpret_cast<const float4*>(csp + 4);
+  const f32x2 cs[4] = {{c_lo.x, c_lo.y}, {c_lo.z, c_lo.w}, {c_hi.x, c_hi.y}, {c_hi.z, c_hi.w}};
+  f32x2 rc[4];
+  bool cs_ok = true;  // false for a zero / tiny / huge / non-finite scale (comparisons fail on NaN)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    rc[k] = f32x2{__builtin_amdgcn_rcpf(cs[k].x), __builtin_amdgcn_rcpf(cs[k].y)};
+    cs_ok &= (fabsf(cs[k].x) >= 0x1.0p-100f) & (fabsf(cs[k].x) <= 0x1.0p+100f) & (fabsf(cs[k].y) >= 0x1.0p-100f) &
+             (fabsf(cs[k].y) <= 0x1.0p+100f);
+  }
+  const QP p = A.p;
+  uint4* dst = reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + rblk * U * upr + cuc;
+  const int nrow = (int)min<int64_t>(U, rows - rblk * U);  // rows of this tile inside the slice
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
+    if (col_ok && u < nrow) st_out<false>(dst, o);
+    dst += upr;
+  }
+}
+
 // --------------------------------------------------------------- single-pass tile path
 // One workgroup per quantization group that is too large (or too 2-D) for a lane group: a
 // BLOCK tile (e.g. FP8_BLOCK 128x128), a CHANNEL row, or a group wider than 512.  The tile
@@ -893,6 +1065,33 @@ FastFn pick_fast(int logl, int kind, bool sym, bool fq, bool nt, bool grp = fals
   }
 }
 
+using FqcFn = void (*)(FastArgs, int64_t);
+template <int LOGL, bool NT>
+FqcFn pick_fqc_kind(int kind, bool sym) {
+  switch (kind) {
+    case K_INT: return sym ? (FqcFn)k_fq_cols<LOGL, K_INT, true, NT> : (FqcFn)k_fq_cols<LOGL, K_INT, false, NT>;
+    case K_FP8: return k_fq_cols<LOGL, K_FP8, true, NT>;
+    case K_MX: return k_fq_cols<LOGL, K_MX, true, NT>;
+    case K_FP4: return k_fq_cols<LOGL, K_FP4, true, NT>;
+    default: return nullptr;  // NVFP4: unit-wise kernel (needs the per-tensor pre-pass)
+  }
+}
+template <bool NT>
+FqcFn pick_fqc_nt(int logl, int kind, bool sym) {
+  switch (logl) {
+    case 0: return pick_fqc_kind<0, NT>(kind, sym);
+    case 1: return pick_fqc_kind<1, NT>(kind, sym);
+    case 2: return pick_fqc_kind<2, NT>(kind, sym);
+    case 3: return pick_fqc_kind<3, NT>(kind, sym);
+    case 4: return pick_fqc_kind<4, NT>(kind, sym);
+    case 5: return pick_fqc_kind<5, NT>(kind, sym);
+    default: return pick_fqc_kind<6, NT>(kind, sym);
+  }
+}
+FqcFn pick_fqc(int logl, int kind, bool sym, bool nt) {
+  return nt ? pick_fqc_nt<true>(logl, kind, sym) : pick_fqc_nt<false>(logl, kind, sym);
+}
+
 using TileFn = void (*)(FastArgs, TileArgs);
 template <int KIND, bool SYM, bool NT>
 TileFn pick_tile_u(int maxu) {
@@ -1167,6 +1366,16 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const bool nt = batch * rows * cols * 2 > (fq ? QZ_NT_BYTES : QZ_NT_BYTES_Q);
+#ifndef QZ_FQ_COLS
+#define QZ_FQ_COLS 1  // column-tiled AWQ fake-quant kernel (0: unit-wise k_group_fast, A/B knob)
+#endif
+    const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS), FBLOCK / WAVE);
+    FqcFn fqc = (QZ_FQ_COLS && fq && col_scales) ? pick_fqc(logl, pl.kind, pl.p.sym != 0, nt) : nullptr;
+    if (fqc && fq_yblocks <= 65535) {
+      hipLaunchKernelGGL(fqc, dim3((unsigned)cdiv(F.units_per_row, WAVE), (unsigned)fq_yblocks, (unsigned)batch),
+                         dim3(FBLOCK), 0, st, F, rows);
+      return launch_err();
+    }
     const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(fq, nt) * WAVE);
     const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),

@@ -9,7 +9,7 @@ OUT=$PWD/gpurun_out/pmck_$TAG
 mkdir -p $OUT
 N=${N:-30}
 timeout -k 5 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $PWD/scripts/kernel_driver.py $N > $OUT/trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $PWD/scripts/kernel_driver.py $N > $OUT/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
 for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE GRBM_COUNT"; do
   n=$(echo $c | tr ' ' '_')

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/pmc_kernels.sh session (gpurun_out/pmck_TAG/) into profiles/ (committed):
+
+  python scripts/pmc_kernels_summary.py TAG
+
+writes profiles/TAG_kernels_stats.csv (the rocprofv3 --kernel-trace --stats summary, torch
+kernel names shortened) and profiles/TAG_kernels_pmc.json: per kernel the median duration from
+the kernel trace, the median of every PMC counter over its launches, HBM bytes per launch
+(MI355X_MICROARCH.md corrections: FETCH_SIZE x2 on gfx950, WRITE_SIZE as-is, KB = 1024 B) next to
+the algorithmic bytes, and the derived issue figures (VALU / VMEM instructions per wave, wave
+lifetime, fraction of wave cycles parked on s_waitcnt vs issuing)."""
+import csv
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+R, C = 11008, 4096
+P = R * C
+T = 16384  # activation tokens of the absmean leg (scripts/kernel_driver.py)
+# kernel-name substring -> (label, algorithmic bytes per launch)
+KERNELS = {
+    "k_group_fast<4, 0, false, true, true, false>": ("quantize int4 g128 (per-weight launch)", int(P * 2.515625)),
+    "k_group_fast<4, 0, true, true, false, false>": ("AWQ fake-quant Q(W*s)/s int4 g128", P * 4 + C * 4),
+    "k_absmean_partial_v8": ("AWQ absmean stage 1 [16384, 4096]", T * C * 2),
+    "k_colsum_final<float>": ("AWQ absmean stage 2", None),
+    "k_wmean_v8": ("AWQ w_mean stage 1", P * 2),
+    "k_colsum_final<double>": ("AWQ w_mean stage 2", None),
+    "k_scale_v8<true>": ("AWQ smoothing W[:, c] *= s[c]", P * 4 + C * 4),
+}
+
+
+def _short(name):
+    return name.split("(")[0][:120] + "(...)" if "at::native" in name else name
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"pmck_{tag}")
+    out = os.path.join(ROOT, "profiles")
+    rows = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_stats.csv"))))
+    with open(os.path.join(out, f"{tag}_kernels_stats.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+        w.writeheader()
+        for r in rows:
+            w.writerow(dict(r, Name=_short(r["Name"])))
+    trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
+    res = {}
+    for sub, (label, alg) in KERNELS.items():
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if sub in r["Kernel_Name"]]
+        if not durs:
+            continue
+        d = {"label": label, "launches": len(durs), "median_ns": statistics.median(durs),
+             "mean_ns": statistics.fmean(durs), "min_ns": min(durs), "counters": {}}
+        for pdir in sorted(os.listdir(src)):
+            p = os.path.join(src, pdir, "run_counter_collection.csv")
+            if pdir == "trace" or not os.path.exists(p):
+                continue
+            by = {}
+            for r in csv.DictReader(open(p)):
+                if sub in r["Kernel_Name"]:
+                    by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+            for c, v in by.items():
+                d["counters"][c] = statistics.median(v)
+        c = d["counters"]
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            d["hbm_bytes"] = c["FETCH_SIZE"] * 1024 * 2 + c["WRITE_SIZE"] * 1024
+        if alg:
+            d["alg_bytes"] = alg
+            d["alg_TBps"] = alg / d["median_ns"] / 1e3
+            d["frac_of_8TBps"] = d["alg_TBps"] / 8.0
+            if "hbm_bytes" in d:
+                d["traffic_over_alg"] = d["hbm_bytes"] / alg
+        if c.get("SQ_WAVES"):
+            wv = c["SQ_WAVES"]
+            d["valu_per_wave"] = c.get("SQ_INSTS_VALU", 0) / wv
+            d["vmem_rd_per_wave"] = c.get("SQ_INSTS_VMEM_RD", 0) / wv
+            d["vmem_wr_per_wave"] = c.get("SQ_INSTS_VMEM_WR", 0) / wv
+            d["salu_per_wave"] = c.get("SQ_INSTS_SALU", 0) / wv
+            d["lds_per_wave"] = c.get("SQ_INSTS_LDS", 0) / wv
+            d["wave_cycles_per_wave_x4"] = c.get("SQ_WAVE_CYCLES", 0) / wv
+        wc = c.get("SQ_WAIT_ANY", 0) + c.get("SQ_WAIT_INST_ANY", 0) + c.get("SQ_ACTIVE_INST_ANY", 0)
+        if wc:
+            d["frac_wait_any"] = c["SQ_WAIT_ANY"] / wc
+            d["frac_wait_inst_any"] = c["SQ_WAIT_INST_ANY"] / wc
+            d["frac_active_inst"] = c["SQ_ACTIVE_INST_ANY"] / wc
+            d["frac_active_valu_of_active"] = c.get("SQ_ACTIVE_INST_VALU", 0) / max(c["SQ_ACTIVE_INST_ANY"], 1)
+        res[label] = d
+    with open(os.path.join(out, f"{tag}_kernels_pmc.json"), "w") as f:
+        json.dump({"source": f"scripts/pmc_kernels.sh TAG={tag} (scripts/kernel_driver.py, 30 launches per kernel, "
+                             "12 rotating [11008, 4096] bf16 copies)", "kernels": res}, f, indent=1)
+    for k, d in res.items():
+        print(f"{k:42s} med {d['median_ns'] / 1e3:7.2f} us  frac {d.get('frac_of_8TBps', 0):.3f}  "
+              f"traffic/alg {d.get('traffic_over_alg', 0):.3f}  valu/wave {d.get('valu_per_wave', 0):7.1f}  "
+              f"wait {d.get('frac_wait_any', 0):.2f} inst-wait {d.get('frac_wait_inst_any', 0):.2f} "
+              f"active {d.get('frac_active_inst', 0):.2f}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

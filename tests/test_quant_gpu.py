@@ -126,6 +126,38 @@ def test_awq_fake_quant_scaled(cuda, scheme):
     _eq(got, ref)
 
 
+@pytest.mark.parametrize("scheme", [SCHEMES[i] for i in (0, 1, 3, 4, 5, 6, 11, 17, 19, 20, 21)], ids=_id)
+@pytest.mark.parametrize("shape", [(333, 768), (7, 4608), (66, 1536)])
+def test_awq_fake_quant_scaled_ragged(cuda, scheme, shape):
+    """The column-tiled fake-quant kernel (k_fq_cols: 4-row tiles, 64-lane column chunks) on
+    shapes whose rows are not a multiple of the tile and whose column units end mid-chunk
+    (768 / 8 = 96 units), with scales spanning several binades and a few tiny/huge columns
+    (the IEEE-division fallback)."""
+    a = QuantizationArgs(**scheme)
+    n, k = shape
+    if k % a.group_size:
+        pytest.skip("columns not divisible by the group size (a ValueError in both)")
+    w = _w(n, k, seed=5)
+    g = torch.Generator().manual_seed(13)
+    s = (2.0 ** (torch.rand(k, generator=g) * 8 - 4)).float()
+    s[3] = 2.0 ** -110
+    s[k // 2] = 2.0 ** 105
+    ref = ct.awq_fake_quant_scaled(w, s, _oracle_args(a))
+    got = ops.fake_quantize(w.to(cuda), a, col_scales=s.to(cuda))
+    _eq(got, ref)
+
+
+def test_awq_fake_quant_scaled_headline_shape(cuda):
+    """Q(W*s)/s of the bench weight [11008, 4096], int4 sym g128, compared in full."""
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    w = _w(11008, 4096, seed=0)
+    g = torch.Generator().manual_seed(3)
+    s = (torch.rand(4096, generator=g) * 3 + 0.05).float()
+    ref = ct.awq_fake_quant_scaled(w, s, _oracle_args(a))
+    got = ops.fake_quantize(w.to(cuda), a, col_scales=s.to(cuda))
+    _eq(got, ref)
+
+
 def test_headline_shape_int4_g128(cuda):
     """The bench workload: bf16 [11008, 4096], int4 sym g128 (compared in full)."""
     w = _w(11008, 4096, seed=0)
