@@ -237,6 +237,25 @@ __device__ __forceinline__ GP group_params(const QP& p, float mn, float mx, floa
   return g;
 }
 
+// calculate_qparams of a symmetric group with a bf16 scale (int / FP8 / native-FP4 kinds) from
+// its absmax: the same result as group_params(p, -am, am, 0, true) with the common case
+// branch-light -- s = bf16(am * (1 / half_range)) when that product is a normal in
+// [2^-120, 2^120] (one unsigned compare on its bits; rcp lemma), else the general routine
+// (zero groups, extreme magnitudes)
+__device__ __forceinline__ GP group_params_sym(const QP& p, float am) {
+  const float q = am * p.inv_half;
+  if (__builtin_expect(__float_as_uint(q) - 0x03800000u <= 0x78000000u, 1)) {
+    GP g;
+    g.sbits = f2bf(q);
+    g.s = bf2f((uint16_t)g.sbits);
+    g.rs = __builtin_amdgcn_rcpf(g.s);
+    g.zp = 0.f;
+    g.fast = true;
+    return g;
+  }
+  return group_params(p, -am, am, 0.f, true);
+}
+
 // quotient of one element (bf16 value x) by the group scale, as compressed-tensors'
 // `x / scale` (bf16 result; f32 for NVFP4).
 __device__ __forceinline__ float qdiv(const QP& p, const GP& g, float x) {

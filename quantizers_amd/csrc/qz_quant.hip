@@ -282,7 +282,12 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       }
       st_out<NTS>(reinterpret_cast<uint4*>(A.q_out) + unit, make_uint4(o[0], o[1], o[2], o[3]));
     } else if (A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
-      // word = sum_i (0x4B000000 + u_i) << 4i  - 0xFB000000   (mod 2^32): one shift-add per code
+      // the low byte of each float 0x4B0000uu is its code u (< 16): gather the even elements'
+      // bytes into E and the odd ones' into O (v_perm_b32), word = E | O << 4 (7 VALU for 8 codes)
+#ifndef QZ_PERM_PACK
+#define QZ_PERM_PACK 1
+#endif
+#if !QZ_PERM_PACK
       uint32_t acc = 0u;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -290,6 +295,13 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         acc += __float_as_uint(q[k].y) << (8 * k + 4);
       }
       st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, acc - 0xFB000000u);
+#else
+      const uint32_t e_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].x), __float_as_uint(q[0].x), 0x0c0c0400u);
+      const uint32_t e_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].x), __float_as_uint(q[2].x), 0x04000c0cu);
+      const uint32_t o_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].y), __float_as_uint(q[0].y), 0x0c0c0400u);
+      const uint32_t o_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].y), __float_as_uint(q[2].y), 0x04000c0cu);
+      st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, ((o_lo | o_hi) << 4) | (e_lo | e_hi));
+#endif
     } else {
       uint32_t c[8];
 #pragma unroll
@@ -410,7 +422,9 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   }
   QP ps = p;
   ps.sym = SYM;
-  const GP g = group_params(ps, mn, mx, gs);
+  // symmetric: mx is the group's absmax
+  const GP g = (SYM && (KIND == K_INT || KIND == K_FP8 || KIND == K_FP4)) ? group_params_sym(ps, mx)
+                                                                          : group_params(ps, mn, mx, gs, SYM);
   if (!valid) return;
   encode_store<KIND, FQ, SYM, NTS>(A, ps, g, x, cs, unit);
   if ((lane & (L - 1)) == 0) {
@@ -466,10 +480,23 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
   FastArgs A = A0;
   int64_t b = blockIdx.y;
   if constexpr (GRP) {  // grouped launch: this workgroup's weight and outputs from the table
+    // table entries are global-memory pointers; casting through address space 1 makes the
+    // compiler emit global_* instead of flat_* loads and stores, which measured SLOWER here
+    // (grouped int4 g128, 100 weights: 17.09 -> 18.16 us/weight, r02g A/B), so flat it stays
+#ifndef QZ_TAB_GLOBAL
+#define QZ_TAB_GLOBAL 0
+#endif
+#if QZ_TAB_GLOBAL
+    A.w = (const uint16_t*)(const __attribute__((address_space(1))) uint16_t*)A0.tab[b];
+    A.q_out = (void*)(__attribute__((address_space(1))) char*)A0.tab[A0.n_tab + b];
+    A.s_out = (void*)(__attribute__((address_space(1))) char*)A0.tab[2 * A0.n_tab + b];
+    A.zp_out = (int8_t*)(__attribute__((address_space(1))) int8_t*)A0.tab[3 * A0.n_tab + b];
+#else
     A.w = reinterpret_cast<const uint16_t*>(A0.tab[b]);
     A.q_out = reinterpret_cast<void*>(A0.tab[A0.n_tab + b]);
     A.s_out = reinterpret_cast<void*>(A0.tab[2 * A0.n_tab + b]);
     A.zp_out = reinterpret_cast<int8_t*>(A0.tab[3 * A0.n_tab + b]);
+#endif
     b = 0;
   }
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
@@ -586,7 +613,7 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
   QP ps = p;
   ps.sym = SYM;
   ps.kind = KIND;
-  const GP g = group_params(ps, mn, mx, 0.f, SYM);
+  const GP g = (SYM && KIND != K_MX) ? group_params_sym(ps, mx) : group_params(ps, mn, mx, 0.f, SYM);
   // quotient x / scale in bf16 (x * rcp(s): rcp lemma)
   f32x2 t[4];
   const f32x2 rs2 = {g.rs, g.rs};

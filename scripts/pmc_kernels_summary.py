@@ -22,7 +22,8 @@ T = 16384  # activation tokens of the absmean leg (scripts/kernel_driver.py)
 # kernel-name substring -> (label, algorithmic bytes per launch)
 KERNELS = {
     "k_group_fast<4, 0, false, true, true, false>": ("quantize int4 g128 (per-weight launch)", int(P * 2.515625)),
-    "k_group_fast<4, 0, true, true, false, false>": ("AWQ fake-quant Q(W*s)/s int4 g128", P * 4 + C * 4),
+    "k_group_fast<4, 0, true, true, false, false>": ("AWQ fake-quant Q(W*s)/s int4 g128 (unit-wise, r02c)", P * 4 + C * 4),
+    "k_fq_cols<4, 0, true, false>": ("AWQ fake-quant Q(W*s)/s int4 g128", P * 4 + C * 4),
     "k_absmean_partial_v8": ("AWQ absmean stage 1 [16384, 4096]", T * C * 2),
     "k_colsum_final<float>": ("AWQ absmean stage 2", None),
     "k_wmean_v8": ("AWQ w_mean stage 1", P * 2),
