@@ -172,6 +172,69 @@ def test_awq_layer_matches_oracle_search(cuda):
         _eq(g_fq, g_ref, f"fake-quant ratio {ratio}")
 
 
+def test_dense_mlp_awq_all_ratios_and_argmin(cuda):
+    """post_attention_layernorm -> {gate, up} (parent: the MLP) through awq_layer: all 20 grid
+    losses against a restatement (oracle statistics, oracle grid scales, oracle Q(W*s)/s, the
+    same MLP forward on the device), the chosen ratio is the restated argmin, and the applied
+    smoothing is bf16(W * s) on gate/up and bf16(w / s) on the norm."""
+    import copy
+    from quantizers_amd.awq import awq_layer
+    from quantizers_amd.oneshot import _batches, _capture_layer0_inputs
+    from quantizers_amd.quantization import QuantizationArgs
+    from quantizers_amd.recipe import AWQMapping
+    m = _qwen3(layers=1).to(cuda)
+    layer = m.model.layers[0]
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    quantized = {f"model.layers.0.mlp.{p}": a for p in ("gate_proj", "up_proj", "down_proj")}
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(_calib(n=3, s=64), None, None, cuda))
+    xs = []
+    h = layer.mlp.register_forward_pre_hook(lambda mod, args: xs.append(args[0].detach().clone()))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    mlp0 = copy.deepcopy(layer.mlp)
+    norm0 = layer.post_attention_layernorm.weight.detach().clone()
+    gw, uw = mlp0.gate_proj.weight.detach().cpu(), mlp0.up_proj.weight.detach().cpu()
+    rep = awq_layer(layer, "model.layers.0", inputs,
+                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized)
+    r = rep["model.layers.0.post_attention_layernorm"]
+    # restatement
+    oa = ct.QArgs(group_size=128)
+    s_ref, n_ref = None, 0
+    for x in xs:
+        (s_ref, n_ref) = ct.awq_accumulate_mean(x.cpu(), None if s_ref is None else (s_ref, n_ref))
+    x_mean = s_ref / n_ref
+    w_mean = ct.awq_layer_means([gw, uw], oa).float()
+    xcat = torch.cat([x.reshape(-1, x.shape[-1]) for x in xs])
+    with torch.no_grad():
+        ref_out = mlp0(xcat)
+        hist = []
+        probe = copy.deepcopy(mlp0)
+        for i in range(20):
+            s = ct.awq_grid_scales(x_mean, w_mean, i / 20, True)
+            probe.gate_proj.weight.copy_(ct.awq_fake_quant_scaled(gw, s, oa))
+            probe.up_proj.weight.copy_(ct.awq_fake_quant_scaled(uw, s, oa))
+            hist.append((ref_out - probe(xcat)).double().pow(2).sum().item() / ref_out.numel())
+    torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(hist), rtol=2e-3, atol=1e-12)
+    best_i = int(round(r["best_ratio"] * 20))
+    want_i = min(range(20), key=lambda i: (hist[i], i))
+    srt = sorted(hist)
+    if srt[1] > srt[0] * 1.002:  # the restated argmin is unambiguous at this tolerance
+        assert best_i == want_i, (best_i, want_i, hist)
+    assert hist[best_i] <= min(hist) * 1.002
+    # the applied smoothing, from the device statistics awq_layer used (same kernels, same order)
+    sums = torch.zeros(x_mean.numel(), dtype=torch.float32, device=cuda)
+    cnt = sum(ops.awq_absmean_accum(x, sums) for x in xs)
+    wsum = torch.zeros(x_mean.numel(), dtype=torch.float64, device=cuda)
+    rows = sum(ops.awq_weight_mean_accum(w.to(cuda), 128, wsum) for w in (gw, uw))
+    torch.testing.assert_close((sums / cnt).cpu(), x_mean, rtol=1e-5, atol=1e-7)
+    s = ops.awq_grid_scales(sums / cnt, (wsum / rows).float(), best_i / 20, True).cpu()
+    _eq(layer.mlp.gate_proj.weight, (gw.float() * s.view(1, -1)).to(torch.bfloat16), "gate smoothed")
+    _eq(layer.mlp.up_proj.weight, (uw.float() * s.view(1, -1)).to(torch.bfloat16), "up smoothed")
+    _eq(layer.post_attention_layernorm.weight, (norm0.cpu().float() / s).to(torch.bfloat16), "norm smoothed")
+
+
 def test_mixed_fp8_block_and_awq(cuda, tmp_path):
     m = _qwen3().to(cuda)
     oneshot(m, os.path.join(ROOT, "configs/recipes/mixed_fp8_block_awq_int4.yaml"), dataset=_calib(),
