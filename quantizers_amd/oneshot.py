@@ -23,7 +23,7 @@ from torch import nn
 from . import awq as awq_mod
 from .model import checkpoint_name, decoder_layers, iter_linears, model_type
 from .quantization import QuantizationScheme
-from .recipe import AWQModifier, QuantizationModifier, match_any, parse_recipe
+from .recipe import AWQModifier, QuantizationModifier, match_any, match_precedence, parse_recipe
 
 log = logging.getLogger(__name__)
 
@@ -33,7 +33,10 @@ class _StopForward(Exception):
 
 
 def resolve_schemes(model: nn.Module, modifiers: List[QuantizationModifier]) -> Dict[str, Tuple[QuantizationScheme, QuantizationModifier]]:
-    """module name -> (scheme, owning modifier); later modifiers do not override earlier ones."""
+    """module name -> (scheme, owning modifier); later modifiers do not override earlier ones.
+    Within a modifier, a module matched by several config groups takes the group of its most
+    specific target, as compressed-tensors resolves overlapping targets: exact name, then
+    ``re:`` regex, then class name (ties: the first group in recipe order)."""
     out: Dict[str, Tuple[QuantizationScheme, QuantizationModifier]] = {}
     refs = iter_linears(model)
     for mod in modifiers:
@@ -42,12 +45,16 @@ def resolve_schemes(model: nn.Module, modifiers: List[QuantizationModifier]) -> 
                 continue
             if match_any(ref.name, ref.type_name, mod.ignore):
                 continue
-            for scheme in mod.config_groups.values():
+            best = None
+            for order, scheme in enumerate(mod.config_groups.values()):
                 if scheme.weights is None:
                     continue
-                if match_any(ref.name, ref.type_name, scheme.targets):
-                    out[ref.name] = (scheme, mod)
-                    break
+                ranks = [r for r in (match_precedence(ref.name, ref.type_name, t) for t in scheme.targets)
+                         if r is not None]
+                if ranks and (best is None or (min(ranks), order) < best[0]):
+                    best = ((min(ranks), order), scheme)
+            if best is not None:
+                out[ref.name] = (best[1], mod)
     return out
 
 

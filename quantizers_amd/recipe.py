@@ -216,3 +216,15 @@ def is_match(name: str, module_type: str, target: str) -> bool:
 
 def match_any(name: str, module_type: str, targets: List[str]) -> bool:
     return any(is_match(name, module_type, t) for t in targets)
+
+
+def match_precedence(name: str, module_type: str, target: str) -> Optional[int]:
+    """compressed-tensors' precedence among the targets a module matches: exact name (0) over
+    ``re:`` regex (1) over class name (2); ``None`` when the target does not match."""
+    if target.startswith("re:"):
+        return 1 if re.match(target[3:], name) is not None else None
+    if target == name:
+        return 0
+    if target == module_type:
+        return 2
+    return None

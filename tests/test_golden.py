@@ -11,7 +11,8 @@ import ct_torch as ct
 import qref
 
 HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-CASES = sorted(f[:-12] for f in os.listdir(HERE) if f.endswith(".safetensors") and f != "inputs.safetensors")
+CASES = sorted(f[:-12] for f in os.listdir(HERE)
+               if f.endswith(".safetensors") and f != "inputs.safetensors" and not f.startswith("awq_"))
 
 
 def _args(case):

@@ -98,6 +98,22 @@ def test_rtn_w4a16_save_roundtrip(cuda, tmp_path):
     _eq(dec["model.layers.0.mlp.down_proj.weight"], ct.dequantize(q, s, None, oa, dtype=torch.bfloat16))
 
 
+def test_documented_patch_keeps_quantization_config(cuda, tmp_path):
+    """INTEGRATION.md's do_oneshot.py patch: save_compressed(model, dir) and then the
+    reference's own model.config.save_pretrained(dir) (e.g. left in by a maintainer) -- the
+    rewritten config.json still carries the compressed-tensors quantization_config."""
+    m = _qwen3(layers=1).to(cuda)
+    oneshot(m, {"s": {"m": {"QuantizationModifier": {"scheme": "W4A16", "targets": "Linear",
+                                                        "ignore": ["lm_head"]}}}})
+    out = str(tmp_path / "ckpt")
+    save_compressed(m, out)
+    want = json.load(open(os.path.join(out, "config.json")))["quantization_config"]
+    m.config.save_pretrained(out)
+    got = json.load(open(os.path.join(out, "config.json")))
+    assert got.get("quantization_config") == want
+    assert want["quant_method"] == "compressed-tensors"
+
+
 def test_awq_int4_g32_end_to_end(cuda, tmp_path):
     torch.manual_seed(0)
     m = _qwen3().to(cuda)

@@ -69,6 +69,34 @@ def test_target_matching():
     assert is_match("model.layers.3.mlp.experts.7.gate_proj", "Linear", "re:.*mlp\\.experts\\.\\d+\\.(down_proj|gate_proj|up_proj)$")
 
 
+def test_overlapping_groups_follow_target_precedence():
+    """A module matched by several config groups takes the most specific target's group
+    (compressed-tensors: exact name > regex > class name), not simply the first group."""
+    from torch import nn
+    from quantizers_amd.oneshot import resolve_schemes
+
+    class Block(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.q_proj = nn.Linear(8, 8, bias=False)
+            self.down_proj = nn.Linear(8, 8, bias=False)
+            self.up_proj = nn.Linear(8, 8, bias=False)
+
+    model = nn.Module()
+    model.layers = nn.ModuleList([Block()])
+    recipe = {"s": {"m": {"QuantizationModifier": {"config_groups": {
+        "group_0": {"targets": ["Linear"], "weights": {"num_bits": 8, "type": "int", "symmetric": True,
+                                                       "strategy": "channel"}},
+        "group_1": {"targets": ["re:.*down_proj$"], "weights": {"num_bits": 4, "type": "int", "symmetric": True,
+                                                               "strategy": "group", "group_size": 8}},
+        "group_2": {"targets": ["layers.0.up_proj", "re:.*up_proj$"],
+                    "weights": {"num_bits": 4, "type": "int", "symmetric": False, "strategy": "group",
+                                "group_size": 8}},
+    }}}}}
+    got = {k: (v[0].weights.num_bits, v[0].weights.symmetric) for k, v in resolve_schemes(model, parse_recipe(recipe)).items()}
+    assert got == {"layers.0.q_proj": (8, True), "layers.0.down_proj": (4, True), "layers.0.up_proj": (4, False)}
+
+
 def test_presets_and_validation():
     s = preset_scheme("W4A16", ["Linear"]).weights
     assert (s.num_bits, s.group_size, s.symmetric) == (4, 128, True)
