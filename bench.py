@@ -461,6 +461,31 @@ def main():
         allgather = {"ms": (time.perf_counter() - ta) * 1e3, "bytes_per_rank": nbytes,
                      "tensors_gathered": len(got), "how": "distributed.gather_state: bucketed all_gather_into_tensor"}
         del got, local_t
+    # PCIe-inclusive rate (not the headline): what save_compressed pays per model on one GPU --
+    # the same plan, then every output tensor copied to pinned host memory (_HostCopier: side
+    # stream, one device->host copy per tensor).  One warm run first (pinned-host allocator).
+    pcie = None
+    if world == 1 and not args.no_extras:
+        from quantizers_amd.compressor import _HostCopier
+
+        def to_host():
+            plan.run(stream)
+            hc = _HostCopier(dev)
+            h = hc.submit(plan.tensors())
+            hc.finish()
+            return h
+
+        to_host()
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        host = to_host()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - tp
+        d2h = sum(t.numel() * t.element_size() for t in host.values())
+        pcie = {"ms": dt * 1e3, "params_per_s": params_step / dt, "d2h_bytes": d2h, "d2h_GBps": d2h / dt / 1e9,
+                "how": "one whole-model CompressionPlan step + device->pinned-host copies of all outputs "
+                       "(compressor._HostCopier), wall clock"}
+        del host
     del plan, units, model
     torch.cuda.empty_cache()
 
@@ -487,6 +512,16 @@ def main():
         value = world * params_step * args.steps / el
         ev_s = ev_ms * 1e-3
         achieved = alg_step * args.steps / ev_s / 1e9
+        # HBM traffic per launch from the committed PMC passes of this same plan
+        # (scripts/pmc_headline.sh -> profiles/headline_pmc.json); null when absent or stale
+        traffic, traffic_src = None, None
+        pmc_path = os.path.join(ROOT, "profiles", "headline_pmc.json")
+        if os.path.exists(pmc_path):
+            pmc = json.load(open(pmc_path))
+            if pmc.get("alg_bytes_per_step") == alg_step and pmc.get("launches_per_step") == launches_step:
+                traffic = pmc["hbm_bytes_per_launch"]
+                traffic_src = (f"profiles/headline_pmc.json ({pmc['tag']}): FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                               f"{pmc['traffic_over_algorithmic']:.4f} x algorithmic")
         line = {
             "metric": METRIC,
             "value": value,
@@ -507,7 +542,7 @@ def main():
                        "parallelism": f"weight-shard dp{world}"},
             "hbm_GBps_step": world * alg_step * args.steps / el / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name(True, 36 * 9728 * 2560 * 2),
                          "kernel_ms_mean": ev_ms / (args.steps * launches_step),
                          "launches_per_step": launches_step, "alg_bytes_per_step": alg_step,
@@ -515,12 +550,12 @@ def main():
                          "kernel_timing": "HIP events on the launch stream around the same K steps as value "
                                           "(K x launches_per_step grouped launches back to back) / launches",
                          "event_ms_per_step": ev_ms / args.steps,
-                         "traffic_note": "per-launch HBM bytes from rocprofv3 PMC passes: profiles/ (pmc_*), "
-                                         "see DESIGN.md §6"},
+                         "traffic_unit": "HBM bytes per launch (alg_bytes_per_launch beside it)"},
             "per_launch": per_launch,
             "cpu_baseline": cpu,
             "parity_check": ok,
             "allgather": allgather,
+            "pcie_inclusive": pcie,
         }
         line.update(extras)
         print(json.dumps(line), flush=True)

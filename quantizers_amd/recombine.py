@@ -104,6 +104,13 @@ def mixed_precision_config(fp8_cfg: dict, compressed_cfg: dict) -> dict:
     return out
 
 
+def output_file_name(fp8_file: str) -> str:
+    """Output shard name of a source shard, as the reference names them
+    (recombine_weights_MiniMax-M2.1.py:68-72, specialised for MiniMax-M2.1: ``...-of-00130``
+    becomes ``...-of-00125``); other names are kept."""
+    return fp8_file.replace("00130", "00125")
+
+
 def recombine(fp8_path: str, compressed_path: str, output_path: str, expert_pattern: str = EXPERT_PATTERN,
               smoothing_pattern: str = SMOOTHING_PATTERN, dry_run: bool = False) -> RecombineStats:
     st = RecombineStats()
@@ -141,10 +148,11 @@ def recombine(fp8_path: str, compressed_path: str, output_path: str, expert_patt
                     merged[name] = f.get_tensor(name)
         st.tensors += len(merged)
         st.bytes += sum(t.numel() * t.element_size() for t in merged.values())
+        out_fn = output_file_name(fn)
         for k in merged:
-            weight_map[k] = fn
+            weight_map[k] = out_fn
         if not dry_run:
-            save_file({k: v.contiguous() for k, v in merged.items()}, os.path.join(output_path, fn),
+            save_file({k: v.contiguous() for k, v in merged.items()}, os.path.join(output_path, out_fn),
                       metadata={"format": "pt"})
     if not dry_run:
         with open(os.path.join(output_path, "model.safetensors.index.json"), "w") as f:

@@ -89,3 +89,26 @@ def test_recombine_dry_run(tmp_path):
     _compressed_ckpt(str(tmp_path / "comp"))
     st = recombine(str(tmp_path / "fp8"), str(tmp_path / "comp"), str(tmp_path / "out"), dry_run=True)
     assert st.experts_replaced == 6 and not (tmp_path / "out").exists()
+
+
+def test_output_shard_names_follow_reference(tmp_path):
+    """recombine_weights_MiniMax-M2.1.py:68-72: MiniMax-M2.1's ``-of-00130`` FP8 shards are
+    written as ``-of-00125``; the index points at the renamed files; other names are kept."""
+    from quantizers_amd.recombine import output_file_name
+    assert output_file_name("model-00007-of-00130.safetensors") == "model-00007-of-00125.safetensors"
+    assert output_file_name("model-00001-of-00002.safetensors") == "model-00001-of-00002.safetensors"
+    src = tmp_path / "fp8"
+    _fp8_ckpt(str(src))
+    idx = json.load(open(src / "model.safetensors.index.json"))
+    for old in ("model-00001-of-00002.safetensors", "model-00002-of-00002.safetensors"):
+        os.rename(src / old, src / old.replace("of-00002", "of-00130"))
+    idx["weight_map"] = {k: v.replace("of-00002", "of-00130") for k, v in idx["weight_map"].items()}
+    json.dump(idx, open(src / "model.safetensors.index.json", "w"))
+    comp = tmp_path / "comp"
+    _compressed_ckpt(str(comp))
+    recombine(str(src), str(comp), str(tmp_path / "out"))
+    files = sorted(f for f in os.listdir(tmp_path / "out") if f.endswith(".safetensors"))
+    assert files == ["model-00001-of-00125.safetensors", "model-00002-of-00125.safetensors"]
+    out_idx = json.load(open(tmp_path / "out" / "model.safetensors.index.json"))
+    assert set(out_idx["weight_map"].values()) == set(files)
+
