@@ -44,7 +44,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 import torch
 from torch import nn
 
-from . import ops
+from . import _lib, ops
 from .model import LinearRef, batch_groups, checkpoint_name, is_fused_experts, iter_linears, stacked_view
 from .quantization import QuantizationArgs
 from .recipe import AWQMapping
@@ -448,6 +448,46 @@ def _expert_batchable(batch: List[ResolvedMapping], quantized: Dict[str, Quantiz
                quantized[r.balance_names[0]] is quantized[r0.balance_names[0]] for r in batch)
 
 
+STATEFUL_OBSERVERS = ("minmax", "static_minmax")
+
+
+class _ObserverState:
+    """Per-balance-layer weight observer memory across the AWQ grid (D7, stateful reading):
+    ``minmax`` = moving average of the group min/max (``averaging_constant``, default 0.01),
+    ``static_minmax`` = running extremes; the first grid point initialises the state.  Updates
+    run in the weight dtype with torch's op order (past + c * (cur - past)), as
+    oracle/ct_torch.moving_average_minmax restates."""
+
+    def __init__(self, a: QuantizationArgs):
+        self.a = a
+        self.c = float((a.observer_kwargs or {}).get("averaging_constant", 0.01))
+        self.mn = self.mx = None
+
+    def update(self, mn: torch.Tensor, mx: torch.Tensor):
+        if self.mn is None:
+            self.mn, self.mx = mn, mx
+        elif self.a.observer == "static_minmax":
+            self.mn, self.mx = torch.minimum(self.mn, mn), torch.maximum(self.mx, mx)
+        else:
+            self.mn = self.mn + self.c * (mn - self.mn)
+            self.mx = self.mx + self.c * (mx - self.mx)
+        return self.mn, self.mx
+
+
+def _fake_quant_stateful(w0: torch.Tensor, a: QuantizationArgs, scales: torch.Tensor, out: torch.Tensor,
+                         st: _ObserverState) -> None:
+    """Q(W*s)/s with qparams from the layer's observer memory: W*s (bf16) -> group min/max
+    (qz_observe_minmax) -> state update -> calculate_qparams -> fake-quantize with those qparams
+    (qz_quantize_qparams, bf16 output, sign of zero kept) -> / s (qz_scale_columns)."""
+    ws = w0.clone()
+    ops.scale_columns_(ws, scales, divide=False)
+    mn, mx = st.update(*ops.observe_minmax(ws, a))
+    scale, zp = ops.calculate_qparams(mn, mx, a)
+    fq = ops.quantize(ws, scale, zp if not a.symmetric else None, a, out_fmt=_lib.QZ_OUT_FAKEQUANT)
+    ops.scale_columns_(fq, scales, divide=True)
+    out.copy_(fq)
+
+
 def _expert_chunk(n_tokens: int, inter: int, hidden: int, budget: int = 4 << 30) -> int:
     """Experts per batched search chunk: their w2 inputs and reference outputs stay resident."""
     per_expert = n_tokens * (inter + hidden) * 2
@@ -457,9 +497,14 @@ def _expert_chunk(n_tokens: int, inter: int, hidden: int, budget: int = 4 << 30)
 @torch.no_grad()
 def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dict]], mappings: List[AWQMapping],
               quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20,
-              mtype: str = "", calibrate_all_experts: bool = True) -> Dict[str, Any]:
+              mtype: str = "", calibrate_all_experts: bool = True,
+              stateful_observers: bool = False) -> Dict[str, Any]:
     """Run AWQ on one decoder layer in place.  ``layer_inputs`` are the cached (args, kwargs)
-    of the layer for every calibration batch.  Returns per-mapping diagnostics."""
+    of the layer for every calibration batch.  Returns per-mapping diagnostics.
+
+    ``stateful_observers``: balance layers whose scheme names the ``minmax`` / ``static_minmax``
+    observer keep that observer's memory across the 20 grid points of their search (D7's
+    stateful reading); default: every observation is memoryless (D7)."""
     resolved = resolve_mappings(layer, prefix, mappings, quantized, mtype)
     if not resolved:
         return {}
@@ -545,12 +590,20 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         tmp = [torch.empty_like(o) for o in orig]
         scales = torch.empty_like(x_mean)
         world, rank = _grid_ranks(grid_shard)
+        obs = [(_ObserverState(quantized[g[0].name])
+                if stateful_observers and quantized[g[0].name].observer in STATEFUL_OBSERVERS else None)
+               for g in groups]
+        if any(o is not None for o in obs):
+            world, rank = 1, 0  # the observer memory runs through the grid in order: no ratio split
         losses = torch.zeros(n_grid, dtype=torch.float64, device=x_mean.device)
         for i in range(rank, n_grid, world):
             ratio = i / n_grid
             ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
-            for g, w0, t in zip(groups, orig, tmp):
-                if len(g) == 1:
+            for g, w0, t, o in zip(groups, orig, tmp, obs):
+                if o is not None:
+                    _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
+                    _view(g).copy_(t)
+                elif len(g) == 1:
                     ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
                 else:
                     ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
@@ -642,7 +695,9 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             continue
         # mutually independent single-layer-parent mappings (e.g. every expert's w3 -> w2):
         # search all (sharded over ranks under torch.distributed), then smooth in order
-        if _expert_batchable(batch, quantized, calibrate_all_experts):
+        stateful = stateful_observers and any(quantized[r.balance_names[0]].observer in STATEFUL_OBSERVERS
+                                              for r in batch)
+        if not stateful and _expert_batchable(batch, quantized, calibrate_all_experts):
             b0 = batch[0].balance[0]
             ei = experts[id(b0.module)]
             n_tok = sum(x.shape[0] for x in ei.x)

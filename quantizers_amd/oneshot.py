@@ -110,7 +110,7 @@ def _layer_out(o):
 
 @torch.no_grad()
 def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report,
-                    calibrate_all_experts: bool = True):
+                    calibrate_all_experts: bool = True, stateful_observers: bool = False):
     layers = decoder_layers(model)
     lname = next(n for n, m in model.named_modules() if m is layers)
     weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
@@ -122,7 +122,8 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
         layer.to(device)
         t0 = time.time()
         rep = awq_mod.awq_layer(layer, checkpoint_name(f"{lname}.{i}", mtype), inputs, mappings, weights,
-                                awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts)
+                                awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts,
+                                stateful_observers=stateful_observers)
         report[f"{lname}.{i}"] = rep
         nxt = []
         for args, kwargs in inputs:
@@ -137,13 +138,15 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
 def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, processor=None,
             max_seq_length: Optional[int] = 2048, num_calibration_samples: Optional[int] = 512,
             moe_calibrate_all_experts: bool = True, device: Union[str, torch.device, None] = None,
-            output_dir: Optional[str] = None, **kwargs) -> nn.Module:
+            output_dir: Optional[str] = None, stateful_observers: bool = False, **kwargs) -> nn.Module:
     """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
     scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
     dataset is already tokenized).  ``moe_calibrate_all_experts``: AWQ statistics and loss
     inputs of expert linears use every calibration token (True, the reference's setting) or
     only the tokens the router sends to that expert (False); the MoE block's own output is
-    always the routed one (awq.py)."""
+    always the routed one (awq.py).  ``stateful_observers``: AWQ grid observations of balance
+    layers whose scheme names ``minmax`` / ``static_minmax`` keep the observer's memory across
+    the grid points (stateful reading); default memoryless (D7)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -161,7 +164,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             # embeddings / rotary / final norm run on the device; layers are onloaded one by one
             _to_device_except(model, decoder_layers(model), device)
         for m in awqs:
-            _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts)
+            _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
+                            stateful_observers)
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
     model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml

@@ -251,6 +251,77 @@ def test_dense_mlp_awq_all_ratios_and_argmin(cuda):
     _eq(layer.post_attention_layernorm.weight, (norm0.cpu().float() / s).to(torch.bfloat16), "norm smoothed")
 
 
+@pytest.mark.parametrize("observer", ["minmax", "static_minmax"])
+def test_stateful_observer_grid(cuda, observer):
+    """D7, stateful reading: a balance layer whose scheme names ``minmax`` (moving average,
+    averaging_constant 0.01) or ``static_minmax`` (running extremes) keeps the observer memory
+    across the grid points.  (1) the device step (W*s -> observe -> state update -> qparams ->
+    fake-quant -> /s) is bit-identical to the oracle over a run of updates; (2) awq_layer's 20
+    losses match a restatement that threads the same state through the grid."""
+    import copy
+    from quantizers_amd.awq import _ObserverState, _fake_quant_stateful, awq_layer
+    from quantizers_amd.oneshot import _batches, _capture_layer0_inputs
+    from quantizers_amd.quantization import QuantizationArgs
+    from quantizers_amd.recipe import AWQMapping
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32, observer=observer)
+    oa = ct.QArgs(group_size=32)
+
+    def step_ref(w, s, past):
+        ws = (w.float() * s.view(1, -1)).to(torch.bfloat16)
+        mn, mx = ct.observe_minmax(ws, oa)
+        if observer == "minmax":
+            mn, mx = ct.moving_average_minmax(mn, mx, *(past or (None, None)))
+        elif past is not None:
+            mn, mx = torch.minimum(past[0], mn), torch.maximum(past[1], mx)
+        sc, zp = ct.calculate_qparams(mn, mx, oa)
+        return (ct.fake_quantize(ws, sc, zp, oa).float() / s.view(1, -1)).to(torch.bfloat16), (mn, mx)
+
+    g = torch.Generator().manual_seed(4)
+    w = (torch.randn(96, 256, generator=g) * 0.02).to(torch.bfloat16)
+    st, past = _ObserverState(a), None
+    out = torch.empty(96, 256, dtype=torch.bfloat16, device=cuda)
+    for i in range(5):
+        s = (torch.rand(256, generator=g) * 2 + 0.2).float()
+        _fake_quant_stateful(w.to(cuda), a, s.to(cuda), out, st)
+        want, past = step_ref(w, s, past)
+        _eq(out, want, f"stateful step {i}")
+        _eq(st.mn, past[0], f"state min {i}")
+    # (2) through awq_layer: post_attention_layernorm -> gate/up, parent the MLP
+    m = _qwen3(layers=1).to(cuda)
+    layer = m.model.layers[0]
+    quantized = {f"model.layers.0.mlp.{p}": a for p in ("gate_proj", "up_proj", "down_proj")}
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(_calib(n=2, s=64), None, None, cuda))
+    xs = []
+    h = layer.mlp.register_forward_pre_hook(lambda mod, args: xs.append(args[0].detach().clone()))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    mlp0 = copy.deepcopy(layer.mlp)
+    gw, uw = mlp0.gate_proj.weight.detach().cpu(), mlp0.up_proj.weight.detach().cpu()
+    rep = awq_layer(layer, "model.layers.0", inputs,
+                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized,
+                    stateful_observers=True)
+    r = rep["model.layers.0.post_attention_layernorm"]
+    sums = torch.zeros(gw.shape[1], dtype=torch.float32, device=cuda)
+    cnt = sum(ops.awq_absmean_accum(x, sums) for x in xs)
+    wsum = torch.zeros(gw.shape[1], dtype=torch.float64, device=cuda)
+    rows = sum(ops.awq_weight_mean_accum(t.to(cuda), 32, wsum) for t in (gw, uw))
+    xcat = torch.cat([x.reshape(-1, x.shape[-1]) for x in xs])
+    hist, pg, pu = [], None, None
+    with torch.no_grad():
+        ref_out = mlp0(xcat)
+        probe = copy.deepcopy(mlp0)
+        for i in range(20):
+            s = ops.awq_grid_scales(sums / cnt, (wsum / rows).float(), i / 20, True).cpu()
+            fg, pg = step_ref(gw, s, pg)
+            fu, pu = step_ref(uw, s, pu)
+            probe.gate_proj.weight.copy_(fg)
+            probe.up_proj.weight.copy_(fu)
+            hist.append((ref_out - probe(xcat)).double().pow(2).sum().item() / ref_out.numel())
+    torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(hist), rtol=1e-3, atol=1e-12)
+
+
 def test_mixed_fp8_block_and_awq(cuda, tmp_path):
     m = _qwen3().to(cuda)
     oneshot(m, os.path.join(ROOT, "configs/recipes/mixed_fp8_block_awq_int4.yaml"), dataset=_calib(),
