@@ -7,14 +7,14 @@ One *step* = one pass of the product's compressor over the whole model: the 252 
 linears (36 layers x q/k/v/o/gate/up/down, 3.63 G params, public Qwen3-4B dims, random bf16
 weights -- there is no checkpoint offline) quantized + packed by ``compressor.CompressionPlan``,
 the exact launch plan ``save_compressed`` runs (same-shape modules of one scheme in ONE grouped
-launch: 7 launches per step).  Weights (7.3 GB) and outputs (1.8 GB) stay resident in HBM, far
+launch: 5 launches per step).  Weights (7.3 GB) and outputs (1.8 GB) stay resident in HBM, far
 larger than the 256 MiB Infinity Cache, so every step streams from HBM; the device->host copy
 that ``save_compressed`` adds is not in the timed region (DESIGN.md §6 gives the
 PCIe-inclusive rate).
 
 ``value`` (params/s) and ``roofline.achieved`` come from the SAME timed region: wall clock
 (barrier + synchronize on both sides, max over ranks) for ``value``; HIP events on the launch
-stream around the same K steps for the kernel time (= the K x 7 launches back to back).  The
+stream around the same K steps for the kernel time (= the K launches back to back).  The
 rocprofv3 kernel trace of the same command is summarised by scripts/prof_summary.py.
 
 Beside it (not the headline): the north-star synthetic weight [11008, 4096] (grouped and one
@@ -436,7 +436,8 @@ def main():
         nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
                                                          for t in o.values() if t is not None)
         us = e0.elapsed_time(e1) * 1e3
-        per_launch.append({"shape": [gq.rows, gq.cols], "weights": gq.n, "us": us, "alg_bytes": nb,
+        per_launch.append({"shapes": sorted({f"{r}x{c}" for r, c in gq.shapes}), "weights": gq.n,
+                           "us": us, "alg_bytes": nb,
                            "GBps": nb / (us * 1e-6) / 1e9})
 
     checks = []

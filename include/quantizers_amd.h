@@ -138,6 +138,21 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
                         const qz_args* a, int32_t out_fmt, qz_stream_t stream);
 
 /*
+ * qz_quantize_grouped_var -- qz_quantize_grouped over n weights of DIFFERENT shapes and one scheme
+ * in ONE launch: every same-scheme linear of a model (Qwen3-4B int4 g128: 252 linears of 5 shapes)
+ * pays the launch ramp and drain once (compressor.CompressionPlan).  Same replaced loop as
+ * qz_quantize_grouped (do_oneshot.py:197).  `rows`, `cols` are HOST arrays [n], validated as
+ * qz_quantize_grouped validates one shape; equal consecutive shapes form a segment and at most 8
+ * segments are allowed (sort the weights by shape), else QZ_ERR_SHAPE.  `table` is the DEVICE
+ * table of qz_quantize_grouped (4*n uint64: weights, codes, scales, zero points or 0), in the
+ * same order.  Outputs exactly qz_quantize's.  n <= 65535.  qz_grouped_blocks(rows, cols) is the
+ * number of workgroups one weight takes in such a launch.
+ */
+int64_t qz_grouped_blocks(int64_t rows, int64_t cols);
+int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* rows, const int64_t* cols,
+                            const qz_args* a, int32_t out_fmt, qz_stream_t stream);
+
+/*
  * qz_quantize_qparams -- quantize with caller-supplied qparams (stateful observers such as the
  * recipes' `minmax`, recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:48).  Replaces [3P]
  * compressed-tensors quantize(x, scale, zero_point, args) / fake_quantize(...).

@@ -29,7 +29,8 @@ EXPORTS = (
     "qz_awq_weight_mean_accum",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
-    "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped",
+    "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
+    "qz_grouped_blocks",
 )
 
 
@@ -65,6 +66,8 @@ def load() -> ctypes.CDLL:
         "qz_quantize": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P, SZ, P], ctypes.c_int),
         "qz_quantize_many": ([I64, P, P, P, P, P, I64, I64, I64, I64, I64, A, I32, P, SZ, P], ctypes.c_int),
         "qz_quantize_grouped": ([I64, P, I64, I64, A, I32, P], ctypes.c_int),
+        "qz_quantize_grouped_var": ([I64, P, P, P, A, I32, P], ctypes.c_int),
+        "qz_grouped_blocks": ([I64, I64], ctypes.c_int64),
         "qz_quantize_qparams": ([P, I64, I64, I64, I64, I64, A, I32, P, P, P, P, P], ctypes.c_int),
         "qz_observe_minmax": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
         "qz_calculate_qparams": ([P, P, I64, A, P, P, P, P], ctypes.c_int),

@@ -128,11 +128,15 @@ def compression_units(model: nn.Module) -> Tuple[List[CompressUnit], Dict[str, t
     return units, raw
 
 
+MIXED_SHAPES = os.environ.get("QZ_PLAN_MIXED", "0") == "1"  # measured slower, see DESIGN §3
+
+
 class CompressionPlan:
     """Prepared kernel launches for a set of compression units whose weights are on ``device``
     (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
-    grouped launch (``ops.GroupedQuantize``: the per-launch ramp paid once per shape, e.g. 7
-    launches for all 252 Qwen3-4B linears); stacked fused experts, FP8_BLOCK, NVFP4 and other
+    grouped launch (``ops.GroupedQuantize``: the launch ramp paid once per shape, 5 launches for
+    all 252 Qwen3-4B linears; one mixed-shape launch per scheme measured 3 % slower, DESIGN §3);
+    stacked fused experts, FP8_BLOCK, NVFP4 and other
     two-pass schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
     friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
 
@@ -150,14 +154,24 @@ class CompressionPlan:
             self.params += w.numel()
             int_q, fmt = ops._compress_plan(a, u.scheme.input_activations is not None)
             if not u.stacked and ops.grouped_ok(a, w):
-                buckets.setdefault((id(u.scheme), tuple(w.shape)), []).append((u, w))
+                # one launch per (scheme, shape); QZ_PLAN_MIXED=1: one launch per scheme over up to
+                # 8 shapes (qz_quantize_grouped_var) -- 3 % slower on Qwen3-4B (r02q A/B)
+                key = (id(u.scheme),) if MIXED_SHAPES else (id(u.scheme), tuple(w.shape))
+                buckets.setdefault(key, []).append((u, w))
             else:
                 self.singles.append((u, w, ops.alloc_outputs(tuple(w.shape), a, fmt, self.device), a, int_q, fmt))
         for items in buckets.values():
             a = items[0][0].scheme.weights
             int_q, fmt = ops._compress_plan(a, items[0][0].scheme.input_activations is not None)
-            for s in range(0, len(items), 65535):
-                part = items[s:s + 65535]
+            if len({tuple(w.shape) for _, w in items}) > 8:  # at most 8 shapes per launch
+                items.sort(key=lambda uw: tuple(uw[1].shape))
+            parts: List[list] = [[]]
+            for uw in items:  # <= 65535 weights and <= 8 shapes per launch
+                cur = parts[-1]
+                if len(cur) == 65535 or (len({tuple(w.shape) for _, w in cur} | {tuple(uw[1].shape)}) > 8):
+                    parts.append([])
+                parts[-1].append(uw)
+            for part in parts:
                 gq = ops.GroupedQuantize([w for _, w in part], a, fmt)
                 self.grouped.append((gq, part, a, int_q, fmt))
 

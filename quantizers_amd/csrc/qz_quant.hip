@@ -61,6 +61,9 @@ __device__ __forceinline__ float grp_min(float v) {
   for (int m = 1; m < L; m <<= 1) v = fminf(v, __shfl_xor(v, m, WAVE));
   return v;
 }
+#ifndef QZ_MAX_SEG
+#define QZ_MAX_SEG 8  // shapes per mixed-shape grouped launch
+#endif
 struct FastArgs {
   const uint16_t* w;
   int64_t n_units;          // batch*rows*cols/8
@@ -77,9 +80,19 @@ struct FastArgs {
   const float* col_scales;  // [cols] (+ b * cs_ld_batch), AWQ prescale (FQ only)
   int64_t cs_ld_batch;      // 0: one scale vector for every slice; cols: one per slice
   // grouped launch (qz_quantize_grouped): device table [4][n_tab] of per-weight pointers
-  // {weight, codes, scale, zero point or 0}; blockIdx.y selects the weight
+  // {weight, codes, scale, zero point or 0}; blockIdx.y selects the weight.  Mixed shapes
+  // (qz_quantize_grouped_var, n_seg > 0): the table holds runs of same-shape weights
+  // ("segments"); segment i covers workgroups [seg_block[i], seg_block[i+1]) of a flat grid,
+  // seg_bpw[i] workgroups per weight (divided by a host-computed magic: scalar ops only),
+  // weights from seg_w0[i], seg_units[i] units each
   const uint64_t* tab;
   int64_t n_tab;
+  int32_t n_seg;
+  uint32_t seg_block[QZ_MAX_SEG + 1];
+  uint32_t seg_bpw[QZ_MAX_SEG];
+  uint32_t seg_magic[QZ_MAX_SEG];  // floor((2^32 - 1) / seg_bpw)
+  uint32_t seg_w0[QZ_MAX_SEG];
+  int64_t seg_units[QZ_MAX_SEG];
 };
 
 // --------------------------------------------------------------- single-pass path
@@ -474,11 +487,27 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
   __shared__ uint4 lds_buf[FBLOCK / WAVE][UNROLL][WAVE];
   const int lane = threadIdx.x & (WAVE - 1);
   const int w = threadIdx.x >> 6;
-  const int64_t tile = (int64_t)blockIdx.x * (FBLOCK / WAVE) + w;
-  const int64_t tiles = (A0.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
-  if (tile >= tiles) return;
   FastArgs A = A0;
   int64_t b = blockIdx.y;
+  int64_t blk = blockIdx.x;
+  if constexpr (GRP) {
+    if (A0.n_seg > 0) {  // mixed shapes: segment, weight and local workgroup (uniform, SALU)
+      const uint32_t x = (uint32_t)blk;
+      int sg = 0;
+#pragma unroll
+      for (int i = 1; i < QZ_MAX_SEG; ++i) sg += (i < A0.n_seg) & (x >= A0.seg_block[i]);
+      const uint32_t rel = x - A0.seg_block[sg], d = A0.seg_bpw[sg];
+      uint32_t q = __umulhi(rel, A0.seg_magic[sg]);  // floor(rel / d) or one less
+      uint32_t r = rel - q * d;
+      if (r >= d) { ++q; r -= d; }
+      b = A0.seg_w0[sg] + q;
+      blk = r;
+      A.units_per_batch = A0.seg_units[sg];
+    }
+  }
+  const int64_t tile = blk * (FBLOCK / WAVE) + w;
+  const int64_t tiles = (A.units_per_batch + UNROLL * WAVE - 1) / (UNROLL * WAVE);
+  if (tile >= tiles) return;
   if constexpr (GRP) {  // grouped launch: this workgroup's weight and outputs from the table
     // table entries are global-memory pointers; casting through address space 1 makes the
     // compiler emit global_* instead of flat_* loads and stores, which measured SLOWER here
@@ -1390,6 +1419,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.cs_ld_batch = cs_ld_batch;
     F.tab = nullptr;
     F.n_tab = 0;
+    F.n_seg = 0;
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const bool nt = batch * rows * cols * 2 > (fq ? QZ_NT_BYTES : QZ_NT_BYTES_Q);
@@ -1438,6 +1468,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       F.cs_ld_batch = 0;
       F.tab = nullptr;
       F.n_tab = 0;
+      F.n_seg = 0;
       TileArgs T;
       T.rows = rows;
       T.tile_rows = th;
@@ -1524,6 +1555,7 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
   F.cs_ld_batch = 0;
   F.tab = table;
   F.n_tab = n;
+  F.n_seg = 0;
   int logl = 0;
   while ((8 << logl) < g) ++logl;
   const bool nt = n * rows * cols * 2 > QZ_NT_BYTES_Q;
@@ -1534,6 +1566,73 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
 #endif
   hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, nt, true), dim3((unsigned)blocks, (unsigned)n),
                      dim3(FBLOCK), QZ_GRP_DYN_LDS, (hipStream_t)stream, F);
+  return launch_err();
+}
+
+int64_t qz_grouped_blocks(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0 || cols % 8) return -1;
+  return cdiv(cdiv(rows * cols / 8, tile_unroll(false, true) * WAVE), FBLOCK / WAVE);
+}
+
+int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* rows, const int64_t* cols,
+                            const qz_args* a, int32_t out_fmt, qz_stream_t stream) {
+  if (n == 0) return QZ_OK;
+  if (n < 0 || n > 65535) return QZ_ERR_SHAPE;
+  if (!table || !rows || !cols || !a) return QZ_ERR_NULL;
+  const int64_t g = a->group_size;
+  const bool grp = a->strategy == QZ_GROUP || a->strategy == QZ_TENSOR_GROUP;
+  const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
+  FastArgs F;
+  F.n_seg = 0;
+  Plan pl;
+  int64_t blocks = 0;
+  for (int64_t i = 0; i < n; ++i) {  // every shape validated as qz_quantize_grouped would
+    if (rows[i] <= 0 || cols[i] <= 0 || cols[i] % 8) return QZ_ERR_SHAPE;
+    int rc = make_plan(a, rows[i], cols[i], &pl);
+    if (rc) return rc;
+    const bool new_seg = i == 0 || rows[i] != rows[i - 1] || cols[i] != cols[i - 1];
+    if (new_seg) {  // runs of equal shapes form the segments
+      if (F.n_seg == QZ_MAX_SEG) return QZ_ERR_SHAPE;
+      const int sgi = F.n_seg++;
+      const int64_t bpw = qz_grouped_blocks(rows[i], cols[i]);
+      F.seg_block[sgi] = (uint32_t)blocks;
+      F.seg_bpw[sgi] = (uint32_t)bpw;
+      F.seg_magic[sgi] = (uint32_t)(0xffffffffull / (uint64_t)bpw);  // q0 >= floor(rel/bpw) - 1
+      F.seg_w0[sgi] = (uint32_t)i;
+      F.seg_units[sgi] = rows[i] * cols[i] / 8;
+    }
+    blocks += qz_grouped_blocks(rows[i], cols[i]);
+    if (blocks > 0x7fffffffLL) return QZ_ERR_SHAPE;
+  }
+  F.seg_block[F.n_seg] = (uint32_t)blocks;
+  for (int i = F.n_seg; i < QZ_MAX_SEG; ++i) {  // unused entries: never selected
+    if (i > F.n_seg) F.seg_block[i] = 0xffffffffu;
+    F.seg_bpw[i] = 1; F.seg_magic[i] = 0xffffffffu; F.seg_w0[i] = 0; F.seg_units[i] = 0;
+  }
+  int rc = check_out_fmt(pl, out_fmt);
+  if (rc) return rc;
+  const bool pack_ok = !(pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits != 4 && a->num_bits != 8);
+  if (!grp || !pow2 || !pack_ok || pl.kind == K_NV || out_fmt == QZ_OUT_FAKEQUANT) return QZ_ERR_FORMAT;
+  if (!aligned(table, 8)) return QZ_ERR_ALIGN;
+  F.w = nullptr;
+  F.n_units = 0;
+  F.units_per_batch = 0;  // per segment
+  F.units_per_row = 0;
+  F.ld_batch = 0;
+  F.p = pl.p;
+  F.out_fmt = out_fmt;
+  F.scale_bytes = pl.scale_bytes;
+  F.q_out = F.s_out = nullptr;
+  F.zp_out = nullptr;
+  F.gscale = nullptr;
+  F.col_scales = nullptr;
+  F.cs_ld_batch = 0;
+  F.tab = table;
+  F.n_tab = n;
+  int logl = 0;
+  while ((8 << logl) < g) ++logl;
+  hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, true, true), dim3((unsigned)blocks, 1),
+                     dim3(FBLOCK), 0, (hipStream_t)stream, F);
   return launch_err();
 }
 

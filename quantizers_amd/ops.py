@@ -204,8 +204,11 @@ def alloc_outputs(shape, a: QuantizationArgs, out_fmt: Optional[int], device) ->
 
 
 class GroupedQuantize:
-    """``qz_quantize_grouped``: n same-shape dense weights quantized in ONE launch (grid.y =
-    weight), the per-launch ramp paid once.  The device pointer table is built once here;
+    """``qz_quantize_grouped``: n dense weights of one scheme quantized in ONE launch, the
+    per-launch ramp paid once.  Same-shape weights: grid.y = weight.  Mixed shapes (up to 8,
+    ``qz_quantize_grouped_var``): one flat grid whose workgroups find their weight from
+    per-shape segments passed as kernel arguments -- a whole model's same-scheme linears in one
+    launch.  The device tables are built once here;
     ``run(stream=None)`` is one ctypes call + one kernel launch.  Outputs are exactly
     ``quantize_weight``'s, one dict per weight (``outs``; allocated when not given)."""
 
@@ -215,37 +218,52 @@ class GroupedQuantize:
             raise ValueError("GroupedQuantize needs at least one weight")
         if len(ws) > 65535:
             raise ValueError("GroupedQuantize: at most 65535 weights per launch")
-        shape = tuple(ws[0].shape)
         for w in ws:
             _check_dev(w, "weight")
-            if tuple(w.shape) != shape or not grouped_ok(a, w) or w.device != ws[0].device:
+            if w.dim() != 2 or not grouped_ok(a, w) or w.device != ws[0].device:
                 raise ValueError("GroupedQuantize: every weight must be a dense, 16-B aligned bf16 [rows, cols] "
-                                 "tensor of one shape on one device, under a single-pass group scheme")
-        r, c = shape
+                                 "tensor on one device, under a single-pass group scheme")
+        shapes = [tuple(w.shape) for w in ws]
+        self.mixed = len(set(shapes)) > 1
         dev = ws[0].device
         self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
         self.ca = a.to_c()
         if outs is None:
-            outs = [alloc_outputs((r, c), a, self.out_fmt, dev) for _ in ws]
+            outs = [alloc_outputs(shp, a, self.out_fmt, dev) for shp in shapes]
         if len(outs) != len(ws):
             raise ValueError("GroupedQuantize: one output dict per weight")
         _check_no_alias(ws, outs)
         if not a.symmetric and any(o.get("zero_point") is None for o in outs):
             raise ValueError("GroupedQuantize: asymmetric schemes need a zero_point output per weight")
         n = len(ws)
-        rows = [[w.data_ptr() for w in ws], [o["codes"].data_ptr() for o in outs],
-                [o["scale"].data_ptr() for o in outs],
-                [0 if o.get("zero_point") is None else o["zero_point"].data_ptr() for o in outs]]
-        self.table = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev)
-        self.n, self.rows, self.cols = n, r, c
-        self.weights, self.outs = list(ws), list(outs)  # keep every pointer alive
         self.lib = _lib.load()
+        # mixed shapes: the table lists equal shapes consecutively (the launch's segments)
+        order = sorted(range(n), key=lambda i: shapes.index(shapes[i])) if self.mixed else list(range(n))
+        rows = [[ws[i].data_ptr() for i in order], [outs[i]["codes"].data_ptr() for i in order],
+                [outs[i]["scale"].data_ptr() for i in order],
+                [0 if outs[i].get("zero_point") is None else outs[i]["zero_point"].data_ptr() for i in order]]
+        if self.mixed:
+            if len(set(shapes)) > 8:
+                raise ValueError("GroupedQuantize: at most 8 distinct shapes per launch")
+            self._rows = (ctypes.c_int64 * n)(*[shapes[i][0] for i in order])
+            self._cols = (ctypes.c_int64 * n)(*[shapes[i][1] for i in order])
+        self.table = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(dev)
+        self.n = n
+        self.rows, self.cols = shapes[0]
+        self.shapes = shapes
+        self.weights, self.outs = list(ws), list(outs)  # keep every pointer alive
 
     def run(self, stream=None) -> List[Dict[str, torch.Tensor]]:
         st = _P(stream.cuda_stream) if stream is not None else _stream()
-        rc = self.lib.qz_quantize_grouped(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
-                                          self.out_fmt, st)
-        _lib.check(rc, "qz_quantize_grouped")
+        if self.mixed:
+            rc = self.lib.qz_quantize_grouped_var(self.n, _ptr(self.table), ctypes.cast(self._rows, _P),
+                                                  ctypes.cast(self._cols, _P), ctypes.byref(self.ca), self.out_fmt,
+                                                  st)
+            _lib.check(rc, "qz_quantize_grouped_var")
+        else:
+            rc = self.lib.qz_quantize_grouped(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
+                                              self.out_fmt, st)
+            _lib.check(rc, "qz_quantize_grouped")
         return self.outs
 
 

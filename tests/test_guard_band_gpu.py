@@ -116,6 +116,25 @@ def test_grouped_quantize_guard_band(cuda):
     assert torch.equal(one["codes"], outs[4]["codes"])
 
 
+def test_grouped_mixed_shapes_guard_band(cuda):
+    """The mixed-shape grouped launch (workgroup -> weight map): nothing outside the outputs."""
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    shapes = [(1024, 2560), (96, 1024), (2560, 512), (8, 128), (640, 2560)]
+    ar = Arena(sum(r * c for r, c in shapes) * 3 + (32 << 20), cuda)
+    ws = [ar.take(shp, torch.bfloat16) for shp in shapes]
+    for i, (w, (r, c)) in enumerate(zip(ws, shapes)):
+        w.copy_(_weights(1, r, c, cuda, seed=i)[0])
+    outs = [{"codes": ar.take((r, c // 8), torch.int32), "scale": ar.take((r, c // 128), torch.bfloat16),
+             "zero_point": None} for r, c in shapes]
+    ops.GroupedQuantize(ws, a, outs=outs).run()
+    torch.cuda.synchronize()
+    ok, where = ar.intact()
+    assert ok, where
+    for i in (0, 3, 4):
+        one = ops.quantize_weight(ws[i], a)
+        assert torch.equal(one["codes"], outs[i]["codes"])
+
+
 def test_awq_stat_kernels_guard_band(cuda):
     T, Cc = 3000, 2560
     ar = Arena(T * Cc * 2 + (32 << 20), cuda)

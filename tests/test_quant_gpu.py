@@ -558,6 +558,27 @@ def test_quantize_grouped_equals_single_calls(cuda, scheme):
         assert torch.equal(o["codes"].cpu(), rf["codes"].cpu())
 
 
+@pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "fp8_g32", "mxfp4_g32"])
+def test_quantize_grouped_mixed_shapes(cuda, scheme):
+    """qz_quantize_grouped_var: weights of different shapes (Qwen3-style q/k/o/gate/down, ragged
+    row counts, a weight smaller than one tile) in ONE launch == quantize_weight per weight."""
+    a = {"int4_g128_sym": QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128),
+         "int4_g32_asym": QuantizationArgs(num_bits=4, type="int", symmetric=False, group_size=32),
+         "fp8_g32": QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32),
+         "mxfp4_g32": QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")}[scheme]
+    shapes = [(512, 2560), (128, 2560), (320, 512), (2560, 1024), (3, 256), (1023, 768), (128, 2560)]
+    ws = [_edge_weight(r, c, a.group_size, seed=s).to(cuda) for s, (r, c) in enumerate(shapes)]
+    gq = ops.GroupedQuantize(ws, a)
+    assert gq.mixed
+    got = gq.run()
+    for w, o in zip(ws, got):
+        rf = ops.quantize_weight(w, a)
+        assert torch.equal(o["codes"].cpu(), rf["codes"].cpu())
+        assert torch.equal(o["scale"].cpu().view(torch.uint8), rf["scale"].cpu().view(torch.uint8))
+        if not a.symmetric:
+            assert torch.equal(o["zero_point"].cpu(), rf["zero_point"].cpu())
+
+
 def test_quantize_grouped_rejects(cuda):
     import ctypes
     nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16)
