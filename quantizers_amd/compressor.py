@@ -129,6 +129,7 @@ def compression_units(model: nn.Module) -> Tuple[List[CompressUnit], Dict[str, t
 
 
 MIXED_SHAPES = os.environ.get("QZ_PLAN_MIXED", "0") == "1"  # measured slower, see DESIGN §3
+PLAN_STREAMS = int(os.environ.get("QZ_PLAN_STREAMS", "1"))  # grouped launches spread over streams (A/B knob)
 
 
 class CompressionPlan:
@@ -143,6 +144,8 @@ class CompressionPlan:
     def __init__(self, units: Sequence[CompressUnit], device):
         self.device = torch.device(device)
         self.grouped = []  # (GroupedQuantize, [(unit, weight)], args, int_q, fmt)
+        self._side = None  # side streams / events of a multi-stream run()
+        self._ev = None
         self.singles = []  # (unit, weight, preallocated outputs, args, int_q, fmt)
         buckets: Dict[tuple, list] = {}
         self.params = 0
@@ -190,8 +193,23 @@ class CompressionPlan:
         return n
 
     def run(self, stream=None) -> None:
-        for gq, *_ in self.grouped:
-            gq.run(stream)
+        main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        n_st = min(PLAN_STREAMS, len(self.grouped))
+        if n_st > 1:  # launches alternate over streams: one launch's drain overlaps the next's fill
+            if self._side is None or len(self._side) != n_st - 1:
+                self._side = [torch.cuda.Stream(self.device) for _ in range(n_st - 1)]
+                self._ev = [torch.cuda.Event() for _ in range(n_st)]
+            self._ev[0].record(main)
+            for sd in self._side:
+                sd.wait_event(self._ev[0])
+            for i, (gq, *_) in enumerate(self.grouped):
+                gq.run(main if i % n_st == 0 else self._side[i % n_st - 1])
+            for sd, ev in zip(self._side, self._ev[1:]):
+                ev.record(sd)
+                main.wait_event(ev)
+        else:
+            for gq, *_ in self.grouped:
+                gq.run(main)
         if self.singles:
             with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device)):
                 for u, w, o, a, int_q, fmt in self.singles:
