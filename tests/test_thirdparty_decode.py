@@ -1,4 +1,4 @@
-"""Third-party pin of the MXFP4 on-disk encoding.
+"""Third-party pins of the on-disk encodings (MXFP4, FP8 group / block / channel, int4 packed words).
 
 compressed-tensors (where the reference's arithmetic lives) is absent, but the image ships an
 independent OCP-MX decoder: transformers' gpt-oss MXFP4 loader
@@ -61,3 +61,91 @@ def test_mxfp4_random_weight_roundtrip():
     s, zp = ct.calculate_qparams(mn, mx, a)
     got = _tf_decode(out["weight_packed"], out["weight_scale"])
     assert torch.equal(got.view(torch.int16), ct.fake_quantize(w, s, zp, a).view(torch.int16))
+
+
+# ---------------------------------------------------------------------------------------------
+# FP8 (group / block / channel) and MXFP4 through a second outside decoder: transformers'
+# fine-grained FP8 dequantizer (``transformers/integrations/finegrained_fp8.py``,
+# ``Fp8Dequantize._dequantize_one``).  It derives the block from the scale grid (rows / scale
+# rows x cols / scale cols), multiplies e4m3 codes (or E2M1 nibbles, low nibble first, with
+# E8M0 scales 2^(byte - 127)) by the block's scale in f32 and rounds to bf16 -- which is
+# compressed-tensors' dequantize for these schemes, so decoding the committed fixtures must give
+# the oracle's fake-quantized weight bit for bit.  This pins the e4m3 code bytes, the scale
+# layout (row-major [N / bh, K / bw]) and the block orientation to outside code.
+fg = pytest.importorskip("transformers.integrations.finegrained_fp8")
+
+FP8_CASES = [("fp8_g32.safetensors", ct.QArgs(num_bits=8, type="float", group_size=32), "weight"),
+             ("fp8_block128.safetensors", ct.QArgs(num_bits=8, type="float", strategy="block",
+                                                   block_structure=(128, 128)), "weight"),
+             ("fp8_channel.safetensors", ct.QArgs(num_bits=8, type="float", strategy="channel"), "weight")]
+
+
+def _fg_decode(codes: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return fg.Fp8Dequantize(None)._dequantize_one(codes, scale, output_dtype=torch.bfloat16)
+
+
+@pytest.mark.parametrize("fixture,a,key", FP8_CASES, ids=["fp8_g32", "fp8_block128", "fp8_channel"])
+@pytest.mark.parametrize("name", ["w_gauss", "w_edge"])
+def test_fp8_golden_decodes_to_oracle_fake_quant(fixture, a, key, name):
+    w = load_file(os.path.join(HERE, "inputs.safetensors"))[name]
+    gold = load_file(os.path.join(HERE, fixture))
+    codes = gold[f"{name}.{key}"].view(torch.float8_e4m3fn)
+    scale = gold[f"{name}.weight_scale"]
+    mn, mx = ct.observe_minmax(w, a)
+    s, zp = ct.calculate_qparams(mn, mx, a)
+    assert torch.equal(s.reshape(scale.shape).view(torch.int16), scale.view(torch.int16))
+    expect = ct.fake_quantize(w, s, zp, a)
+    got = _fg_decode(codes, scale)
+    assert torch.equal(got.view(torch.int16), expect.view(torch.int16))
+
+
+@pytest.mark.parametrize("name", ["w_gauss", "w_edge"])
+def test_mxfp4_golden_decodes_with_finegrained_dequant(name):
+    a = ct.QArgs(num_bits=4, type="float", group_size=32, scale_dtype="e8m0")
+    w = load_file(os.path.join(HERE, "inputs.safetensors"))[name]
+    gold = load_file(os.path.join(HERE, "mxfp4_g32.safetensors"))
+    packed, scale = gold[f"{name}.weight_packed"], gold[f"{name}.weight_scale"]
+    mn, mx = ct.observe_minmax(w, a)
+    s, zp = ct.calculate_qparams(mn, mx, a)
+    got = _fg_decode(packed.view(torch.int8), scale.view(torch.uint8))
+    assert torch.equal(got.view(torch.int16), ct.fake_quantize(w, s, zp, a).view(torch.int16))
+
+
+# ---------------------------------------------------------------------------------------------
+# int4 pack-quantized words through a third outside decoder: transformers' Metal affine
+# dequantizer (``transformers/integrations/metal_quantization.py``,
+# ``_affine_dequantize_tensor``: element i of a 32-bit word at bits 4i, word k of a row holding
+# columns 8k..8k+7, value = u * scale + bias per group).  compressed-tensors' symmetric int4 value
+# (u - 8) * s is that affine form with bias = -8 s (exact in f32), the asymmetric one
+# (u - 8 - zp) * s with bias = (-8 - zp) s; the zero points (packed along dim 0, D2) are unpacked
+# by the same routine on the transposed words.  Pins the nibble order, the word layout and the +8
+# offset of pack_to_int32 to outside code.
+metal = pytest.importorskip("transformers.integrations.metal_quantization")
+
+
+def _metal_unpack_codes(words: torch.Tensor) -> torch.Tensor:
+    """[R, W] int32 words -> [R, 8 W] unsigned nibbles via the Metal decoder (scale 1, bias 0)."""
+    r, wcols = words.shape  # one group per row: scale 1, bias 0
+    return metal._affine_dequantize_tensor(words, torch.ones(r, 1), torch.zeros(r, 1), wcols * 8, 4)
+
+
+@pytest.mark.parametrize("fixture,group,sym", [("int4_sym_g128", 128, True), ("int4_sym_g32", 32, True),
+                                               ("int4_asym_g128", 128, False), ("int4_asym_g32", 32, False)])
+@pytest.mark.parametrize("name", ["w_gauss", "w_edge"])
+def test_int4_packed_golden_decodes_with_metal_affine_dequant(fixture, group, sym, name):
+    a = ct.QArgs(num_bits=4, group_size=group, symmetric=sym)
+    w = load_file(os.path.join(HERE, "inputs.safetensors"))[name]
+    gold = load_file(os.path.join(HERE, f"{fixture}.safetensors"))
+    packed, scale = gold[f"{name}.weight_packed"], gold[f"{name}.weight_scale"].float()
+    n = packed.shape[0]
+    if sym:
+        zp = torch.zeros_like(scale)
+    else:  # zero points packed along dim 0: unpack the transposed words with the same decoder
+        zpk = gold[f"{name}.weight_zero_point"]
+        zp = (_metal_unpack_codes(zpk.t().contiguous()).t()[:n] - 8)
+    got = metal._affine_dequantize_tensor(packed, scale, (-8.0 - zp) * scale, group, 4).to(torch.bfloat16)
+    mn, mx = ct.observe_minmax(w, a)
+    s, z = ct.calculate_qparams(mn, mx, a)
+    expect = ct.fake_quantize(w, s, z, a)
+    # the decoders cannot produce -0 (u * s + b); the oracle's fake-quant keeps torch.round's sign
+    assert torch.equal(got.float(), expect.float())
