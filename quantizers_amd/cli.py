@@ -49,6 +49,8 @@ def parse_args(argv=None):
     p.add_argument("--calib-random", type=str, default=None, help="N,S synthetic calibration tokens")
     p.add_argument("--max-seq-length", type=int, default=None)
     p.add_argument("--device", type=str, default=None)
+    p.add_argument("--stateful-observers", action="store_true",
+                   help="AWQ grid: minmax/static_minmax observers keep memory across grid points (DESIGN D7)")
     return p.parse_args(argv)
 
 
@@ -110,9 +112,32 @@ def _rank() -> int:
     return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
 
 
+def _init_distributed(args) -> bool:
+    """Under torchrun (WORLD_SIZE > 1): one process per GPU -- pin this rank's device and join the
+    process group (RCCL) so oneshot splits the AWQ searches and save_compressed shards the
+    compression over the ranks (rank 0 writes).  Returns True when this call created the group."""
+    import torch
+    import torch.distributed as dist
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1 or dist.is_initialized():
+        return False
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("QZ_DIST_BACKEND", "nccl")  # gloo: rehearsal with ranks sharing a GPU
+    if backend == "gloo":
+        local %= max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(local)
+    if args.device is None:
+        args.device = f"cuda:{local}"
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return True
+
+
 def main(argv=None):
     args = parse_args(argv)
     setup_logging(args.log_file, logging.DEBUG if args.debug else logging.INFO)
+    own_group = _init_distributed(args)
     from .config import load_run_config
     from .oneshot import oneshot
     from .compressor import save_compressed
@@ -130,7 +155,7 @@ def main(argv=None):
     t0 = time.time()
     oneshot(model=model, recipe=recipe_path, dataset=dataset, max_seq_length=max_len,
             num_calibration_samples=len(dataset) if dataset else None, moe_calibrate_all_experts=True,
-            device=args.device)
+            device=args.device, stateful_observers=args.stateful_observers)
     logging.info("Completed quantization in %.2f seconds", time.time() - t0)
     if _rank() == 0:
         os.makedirs("outputs", exist_ok=True)
@@ -141,6 +166,9 @@ def main(argv=None):
         tokenizer.save_pretrained(output_dir)
     logging.info("Saved quantized model in %.2f seconds", time.time() - t0)
     logging.info("SUCCESS: Quantized model saved in %s", output_dir)
+    if own_group:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return output_dir
 
 

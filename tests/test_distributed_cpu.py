@@ -41,7 +41,12 @@ def _worker(rank, world, port, q):
         return ct.compress_weight(w, a)
 
     out = sharded_compress(_weights(), compress, device=torch.device("cpu"))
-    q.put((rank, calls, {k: v.clone() for k, v in out.items()}))
+    # tensors travel as serialized bytes: a tensor put on the queue is shared through a file
+    # descriptor of this process, which may have exited before the parent unpickles it
+    import io
+    buf = io.BytesIO()
+    torch.save({k: v.clone() for k, v in out.items()}, buf)
+    q.put((rank, calls, buf.getvalue()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -70,7 +75,8 @@ def test_sharded_compress_gloo_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    res.sort()
+    import io
+    res = sorted((r, c, torch.load(io.BytesIO(b), weights_only=True)) for r, c, b in res)
     calls0, calls1 = res[0][1], res[1][1]
     assert not set(calls0) & set(calls1) and sorted(calls0 + calls1) == sorted(_weights())
     ref = {}
