@@ -177,10 +177,13 @@ int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
   return cdiv(T, *tc);
 }
 
-// row chunks of the w_mean stage 1: >= 16 rows each (4 per wave), about 1024 workgroups
+#ifndef QZ_WMEAN_BLOCKS
+#define QZ_WMEAN_BLOCKS 1024  // tuning knob: target stage-1 workgroups of w_mean
+#endif
+// row chunks of the w_mean stage 1: >= 16 rows each (4 per wave), about QZ_WMEAN_BLOCKS workgroups
 int64_t wmean_chunks(int64_t R, int64_t C, int64_t* rc) {
   const int64_t bx = cdiv(C, 512);
-  const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, 16), cdiv(1024, bx)));
+  const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, 16), cdiv(QZ_WMEAN_BLOCKS, bx)));
   *rc = cdiv(R, nrc);
   return cdiv(R, *rc);
 }

@@ -138,7 +138,8 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
 def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, processor=None,
             max_seq_length: Optional[int] = 2048, num_calibration_samples: Optional[int] = 512,
             moe_calibrate_all_experts: bool = True, device: Union[str, torch.device, None] = None,
-            output_dir: Optional[str] = None, stateful_observers: bool = False, **kwargs) -> nn.Module:
+            output_dir: Optional[str] = None, stateful_observers: bool = False,
+            device_resident: Optional[bool] = None, **kwargs) -> nn.Module:
     """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
     scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
     dataset is already tokenized).  ``moe_calibrate_all_experts``: AWQ statistics and loss
@@ -146,7 +147,11 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     only the tokens the router sends to that expert (False); the MoE block's own output is
     always the routed one (awq.py).  ``stateful_observers``: AWQ grid observations of balance
     layers whose scheme names ``minmax`` / ``static_minmax`` keep the observer's memory across
-    the grid points (stateful reading); default memoryless (D7)."""
+    the grid points (stateful reading); default memoryless (D7).
+    ``device_resident``: a host-resident model is moved to ``device`` for the AWQ pass and left
+    there (True), or only its decoder layers are onloaded one at a time and returned to the host
+    (False, the reference's placement); default: resident when its parameters take at most
+    half of the device's free memory."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -161,8 +166,14 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         if not batches:
             raise ValueError("AWQModifier needs a calibration dataset")
         if next(model.parameters()).device.type == "cpu":
-            # embeddings / rotary / final norm run on the device; layers are onloaded one by one
-            _to_device_except(model, decoder_layers(model), device)
+            if device_resident if device_resident is not None else _fits_on_device(model, device):
+                # 288 GB of HBM: a model that fits moves to the device once and stays there (no
+                # per-layer onload / offload over PCIe; save_compressed then needs no staging)
+                _to_device_staged(model, device)
+            else:
+                # embeddings / rotary / final norm run on the device; layers are onloaded one
+                # by one (the reference's sequential-pipeline placement)
+                _to_device_except(model, decoder_layers(model), device)
         for m in awqs:
             _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
                             stateful_observers)
@@ -174,6 +185,48 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         from .compressor import save_compressed
         save_compressed(model, output_dir)
     return model
+
+
+@torch.no_grad()
+def _to_device_staged(model: nn.Module, device, chunk_bytes: int = 256 << 20) -> None:
+    """Host -> device move of every parameter / buffer through two pinned staging buffers (host
+    memcpy of chunk k+1 overlaps the DMA of chunk k on a side stream) instead of one pageable
+    copy per tensor: the Qwen3-4B random-init model's 8 GB took 7.8 s as ``model.to(device)``."""
+    device = torch.device(device)
+    st = torch.cuda.Stream(device)
+    stage = [torch.empty(chunk_bytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    done: List[Optional[torch.cuda.Event]] = [None, None]
+    k = 0
+    for m in model.modules():
+        for store in (m._parameters, m._buffers):
+            for name, t in list(store.items()):
+                if t is None or t.device.type != "cpu":
+                    continue
+                src = t.detach().contiguous()
+                dst = torch.empty(src.shape, dtype=src.dtype, device=device)
+                sb, db = src.reshape(-1).view(torch.uint8), dst.reshape(-1).view(torch.uint8)
+                for off in range(0, sb.numel(), chunk_bytes):
+                    n = min(chunk_bytes, sb.numel() - off)
+                    i = k % 2
+                    if done[i] is not None:
+                        done[i].synchronize()  # the DMA that last read this staging buffer
+                    stage[i][:n].copy_(sb[off:off + n])
+                    with torch.cuda.stream(st):
+                        db[off:off + n].copy_(stage[i][:n], non_blocking=True)
+                        done[i] = torch.cuda.Event()
+                        done[i].record(st)
+                    k += 1
+                if isinstance(t, nn.Parameter):
+                    t.data = dst
+                else:
+                    store[name] = dst
+    st.synchronize()
+
+
+def _fits_on_device(model: nn.Module, device) -> bool:
+    nbytes = sum(p.numel() * p.element_size() for p in model.parameters())
+    free, _ = torch.cuda.mem_get_info(torch.device(device))
+    return nbytes <= free // 2
 
 
 def _to_device_except(model: nn.Module, layers: nn.ModuleList, device):

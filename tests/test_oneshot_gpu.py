@@ -114,6 +114,23 @@ def test_documented_patch_keeps_quantization_config(cuda, tmp_path):
     assert want["quant_method"] == "compressed-tensors"
 
 
+def test_host_model_resident_vs_layer_onload(cuda):
+    """A host-resident model: moved to the device once (device_resident=True, the default when it
+    fits) or onloaded layer by layer and returned to the host (False, the reference's placement)
+    -- the smoothed weights and the compressed tensors are identical either way."""
+    recipe = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g32.yaml")
+    out = {}
+    for resident in (True, False):
+        m = _qwen3()
+        oneshot(m, recipe, dataset=_calib(), max_seq_length=64, device=cuda, device_resident=resident)
+        dev = next(m.model.layers[0].parameters()).device
+        assert dev.type == ("cuda" if resident else "cpu")
+        out[resident] = compressed_state_dict(m)
+    assert out[True].keys() == out[False].keys()
+    for k in out[True]:
+        _eq(out[True][k], out[False][k], k)
+
+
 def test_awq_int4_g32_end_to_end(cuda, tmp_path):
     torch.manual_seed(0)
     m = _qwen3().to(cuda)
