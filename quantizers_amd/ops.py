@@ -238,7 +238,10 @@ class GroupedQuantize:
         n = len(ws)
         self.lib = _lib.load()
         # mixed shapes: the table lists equal shapes consecutively (the launch's segments)
-        order = sorted(range(n), key=lambda i: shapes.index(shapes[i])) if self.mixed else list(range(n))
+        first: Dict[tuple, int] = {}
+        for i, shp in enumerate(shapes):
+            first.setdefault(shp, i)
+        order = sorted(range(n), key=lambda i: first[shapes[i]]) if self.mixed else list(range(n))
         rows = [[ws[i].data_ptr() for i in order], [outs[i]["codes"].data_ptr() for i in order],
                 [outs[i]["scale"].data_ptr() for i in order],
                 [0 if outs[i].get("zero_point") is None else outs[i]["zero_point"].data_ptr() for i in order]]
