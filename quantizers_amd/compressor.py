@@ -169,11 +169,14 @@ class CompressionPlan:
             if len({tuple(w.shape) for _, w in items}) > 8:  # at most 8 shapes per launch
                 items.sort(key=lambda uw: tuple(uw[1].shape))
             parts: List[list] = [[]]
+            seen: set = set()
             for uw in items:  # <= 65535 weights and <= 8 shapes per launch
-                cur = parts[-1]
-                if len(cur) == 65535 or (len({tuple(w.shape) for _, w in cur} | {tuple(uw[1].shape)}) > 8):
+                shp = tuple(uw[1].shape)
+                if len(parts[-1]) == 65535 or (shp not in seen and len(seen) == 8):
                     parts.append([])
+                    seen = set()
                 parts[-1].append(uw)
+                seen.add(shp)
             for part in parts:
                 gq = ops.GroupedQuantize([w for _, w in part], a, fmt)
                 self.grouped.append((gq, part, a, int_q, fmt))
