@@ -133,12 +133,22 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
 #endif
 
-// round both lanes of an f32 pair to bf16 (one v_cvt_pk_bf16_f32) and widen back
+// round both lanes of an f32 pair to bf16 and widen back.  QZ_BFR_ZERO_HI: one
+// v_cvt_pk_bf16_f32(0, v) per lane puts bf16(v) in the HIGH half over a zero low half -- the f32
+// value bf16(v) itself -- so 2 VALU per pair instead of a packed convert + 2 unpacks (3)
+#ifndef QZ_BFR_ZERO_HI
+#define QZ_BFR_ZERO_HI 1
+#endif
 __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
-  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
   f32x2 r;
+#if QZ_BFR_ZERO_HI
+  r.x = __uint_as_float(__builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){0.0f, v.x}, bf16x2)));
+  r.y = __uint_as_float(__builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){0.0f, v.y}, bf16x2)));
+#else
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
   r.x = __uint_as_float(u << 16);
   r.y = __uint_as_float(u & 0xffff0000u);
+#endif
   return r;
 }
 
@@ -653,7 +663,7 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
     for (int k = 0; k < 4; ++k) { t[k].x = x[k].x / g.s; t[k].y = x[k].y / g.s; }
   }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) t[k] = unpk(pk_bf16(t[k]));
+  for (int k = 0; k < 4; ++k) t[k] = bfr2(t[k]);
   const f32x2 s2 = {g.s, g.s};
   f32x2 dq[4];
   if (KIND == K_INT) {
@@ -661,11 +671,11 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       f32x2 tk = t[k];
-      if (!SYM) tk = unpk(pk_bf16(tk + zp2));
+      if (!SYM) tk = bfr2(tk + zp2);
       const f32x2 r = {__builtin_rintf(__builtin_amdgcn_fmed3f(tk.x, p.qmin, p.qmax)),
                        __builtin_rintf(__builtin_amdgcn_fmed3f(tk.y, p.qmin, p.qmax))};
       // symmetric: the zero point is 0 and r - 0 == r exactly (sign of zero kept)
-      dq[k] = SYM ? unpk(pk_bf16(r * s2)) : unpk(pk_bf16(unpk(pk_bf16(r - zp2)) * s2));
+      dq[k] = SYM ? bfr2(r * s2) : bfr2(bfr2(r - zp2) * s2);
     }
   } else {
 #pragma unroll
