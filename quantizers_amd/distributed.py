@@ -86,6 +86,13 @@ def gather_state(local: Dict[str, torch.Tensor], device=None, dst: Optional[int]
         if not to_host:
             return dict(local)
         return {k: (v.cpu() if v.is_cuda else v) for k, v in local.items()}
+    return _gather_packed(local, device, dst, to_host, bucket_bytes)
+
+
+def _gather_packed(local: Dict[str, torch.Tensor], device, dst: Optional[int], to_host: bool,
+                   bucket_bytes: int) -> Dict[str, torch.Tensor]:
+    """gather_state's collective path (any world size, so a 1-rank RCCL group exercises it)."""
+    world = dist.get_world_size()
     rank = dist.get_rank()
     nccl = dist.get_backend() == "nccl"
     if device is None:

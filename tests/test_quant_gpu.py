@@ -597,3 +597,44 @@ def test_quantize_grouped_rejects(cuda):
     with pytest.raises(ValueError):  # output aliasing a weight
         ops.GroupedQuantize([w], a, outs=[{"codes": w.view(torch.int32)[:, :32], "scale": w[:, :2],
                                            "zero_point": None}])
+
+
+def test_reentrant_from_host_threads(cuda):
+    """The ABI is stateless and reentrant (include/quantizers_amd.h): four host threads, each on
+    its own stream, quantize / fake-quantize / grouped-quantize concurrently -- every result equals
+    the serial one."""
+    import threading
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    ws = [_edge_weight(512, 1024, 128, seed=40 + i).to(cuda) for i in range(4)]
+    s = (torch.rand(1024, generator=torch.Generator().manual_seed(2)) + 0.5).to(cuda)
+    ref = [(ops.quantize_weight(w, a), ops.fake_quantize(w, a, col_scales=s)) for w in ws]
+    ref_g = ops.GroupedQuantize(ws, a).run()
+    torch.cuda.synchronize()
+    got, errs = [None] * 4, []
+
+    def work(i):
+        try:
+            st = torch.cuda.Stream(cuda)
+            with torch.cuda.stream(st):
+                outs = []
+                for _ in range(5):
+                    outs.append((ops.quantize_weight(ws[i], a), ops.fake_quantize(ws[i], a, col_scales=s),
+                                 ops.GroupedQuantize(ws, a).run(st)))
+            st.synchronize()
+            got[i] = outs
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for i in range(4):
+        for q, fq, g in got[i]:
+            _eq(q["codes"], ref[i][0]["codes"])
+            _eq(q["scale"], ref[i][0]["scale"])
+            _eq(fq, ref[i][1])
+            for o, r in zip(g, ref_g):
+                _eq(o["codes"], r["codes"])
