@@ -141,7 +141,7 @@ class CompressionPlan:
     two-pass schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
     friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
 
-    def __init__(self, units: Sequence[CompressUnit], device):
+    def __init__(self, units: Sequence[CompressUnit], device, stager=None):
         self.device = torch.device(device)
         self.grouped = []  # (GroupedQuantize, [(unit, weight)], args, int_q, fmt)
         self._side = None  # side streams / events of a multi-stream run()
@@ -149,11 +149,16 @@ class CompressionPlan:
         self.singles = []  # (unit, weight, preallocated outputs, args, int_q, fmt)
         buckets: Dict[tuple, list] = {}
         self.params = 0
+        staged = False
         for u in units:
             a = u.scheme.weights
             w = u.view()
-            if w.device != self.device:
-                w = w.to(self.device)
+            if w.device != self.device:  # host-resident weight: pinned, double-buffered staging
+                if stager is None:
+                    from .staging import H2DStager
+                    stager = H2DStager(self.device)
+                w = stager.copy(w)
+                staged = True
             self.params += w.numel()
             int_q, fmt = ops._compress_plan(a, u.scheme.input_activations is not None)
             if not u.stacked and ops.grouped_ok(a, w):
@@ -180,6 +185,10 @@ class CompressionPlan:
             for part in parts:
                 gq = ops.GroupedQuantize([w for _, w in part], a, fmt)
                 self.grouped.append((gq, part, a, int_q, fmt))
+        self._ready = None  # completion of the staging copies: every run() waits for it
+        if staged:
+            self._ready = torch.cuda.Event()
+            self._ready.record(stager.stream)
 
     @property
     def launches(self) -> int:
@@ -197,6 +206,8 @@ class CompressionPlan:
 
     def run(self, stream=None) -> None:
         main = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if self._ready is not None:
+            main.wait_event(self._ready)
         n_st = min(PLAN_STREAMS, len(self.grouped))
         if n_st > 1:  # launches alternate over streams: one launch's drain overlaps the next's fill
             if self._side is None or len(self._side) != n_st - 1:
@@ -339,8 +350,12 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
         mine = [u for i, u in enumerate(units) if i in keep]
     copier = _HostCopier(device) if (to_host and world == 1 and device.type == "cuda") else None
     local: Dict[str, torch.Tensor] = {}
+    stager = None
+    if device.type == "cuda" and any(u.refs[0].weight.device != device for u in mine):
+        from .staging import H2DStager
+        stager = H2DStager(device)  # one pair of pinned buffers for every chunk
     for chunk in _chunks(mine, STAGE_BYTES, device):
-        plan = CompressionPlan(chunk, device)
+        plan = CompressionPlan(chunk, device, stager)
         plan.run()
         t = plan.tensors()
         local.update(copier.submit(t) if copier is not None else t)

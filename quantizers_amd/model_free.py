@@ -7,7 +7,7 @@ Every floating 2-D ``<module>.weight`` tensor whose module name is not matched b
 is a quantization target (a checkpoint has no module types; the reference's ignore list names
 the non-Linear 2-D tensors such as ``model.embed_tokens``).  Per shard file:
 
-  disk --(reader threads, mmap)--> host --H2D--> fused HIP quantize+pack (ops.compress_weights:
+  disk --(reader threads, mmap)--> host --H2D (pinned staging)--> fused HIP quantize+pack (ops.compress_weights:
        the file's same-shape weights in one grouped launch) --async D2H, pinned--> host
        --(writer threads, after the copy event)--> disk
 
@@ -42,6 +42,7 @@ from .compressor import _HostCopier, quantization_config_for
 from .distributed import plan_shards
 from .quantization import QuantizationArgs, QuantizationScheme, preset_scheme
 from .recipe import match_any
+from .staging import H2DStager
 
 log = logging.getLogger(__name__)
 
@@ -95,8 +96,9 @@ def _read(path: str) -> Dict[str, torch.Tensor]:
 
 
 def _quantize_file(tensors: Dict[str, torch.Tensor], sch: QuantizationScheme, ignore: List[str], device,
-                   quantized: List[str], skipped: List[str], copier=None) -> Dict[str, torch.Tensor]:
-    """One shard's output tensors.  Every target of the file goes to the device, then ONE
+                   quantized: List[str], skipped: List[str], copier=None, stager=None) -> Dict[str, torch.Tensor]:
+    """One shard's output tensors.  Every target of the file goes to the device (through the
+    pinned staging buffers of ``stager`` when given), then ONE
     ``ops.compress_weights`` call quantizes them (same-shape weights in one grouped launch);
     with ``copier`` the compressed tensors come back through pinned memory asynchronously (valid
     once the copier's last event completes)."""
@@ -119,9 +121,11 @@ def _quantize_file(tensors: Dict[str, torch.Tensor], sch: QuantizationScheme, ig
             out[name] = t
             continue
         mods.append(mod)
-        ws.append(t.to(device, non_blocking=True))
+        ws.append(stager.copy(t) if stager is not None else t.to(device))
     if not ws:
         return out
+    if stager is not None:
+        stager.wait()  # the quantize launches (current stream) see the staged weights
     comps = ops.compress_weights(ws, a, has_activation_quant=sch.input_activations is not None)
     dev_out = {f"{mod}.{k}": v for mod, comp in zip(mods, comps) for k, v in comp.items()}
     if copier is not None:
@@ -169,11 +173,12 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
         reads = [pool.submit(_read, os.path.join(model_stub, f)) for f in mine[:2]]
         writes = []
         copier = _HostCopier(device)
+        stager = H2DStager(device)
         for i, fn in enumerate(mine):
             tensors = reads[i].result()
             if i + 2 < len(mine):
                 reads.append(pool.submit(_read, os.path.join(model_stub, mine[i + 2])))
-            out = _quantize_file(tensors, sch, ignore, device, quantized, skipped, copier)
+            out = _quantize_file(tensors, sch, ignore, device, quantized, skipped, copier, stager)
             ready = copier.last_event
             for k, t in out.items():
                 weight_map[k] = fn

@@ -188,34 +188,18 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
 
 
 @torch.no_grad()
-def _to_device_staged(model: nn.Module, device, chunk_bytes: int = 256 << 20) -> None:
-    """Host -> device move of every parameter / buffer through two pinned staging buffers (host
-    memcpy of chunk k+1 overlaps the DMA of chunk k on a side stream) instead of one pageable
-    copy per tensor: the Qwen3-4B random-init model's 8 GB took 7.8 s as ``model.to(device)``."""
-    device = torch.device(device)
-    st = torch.cuda.Stream(device)
-    stage = [torch.empty(chunk_bytes, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
-    done: List[Optional[torch.cuda.Event]] = [None, None]
-    k = 0
+def _to_device_staged(model: nn.Module, device) -> None:
+    """Host -> device move of every parameter / buffer through pinned staging buffers
+    (``staging.H2DStager``) instead of one pageable copy per tensor: the Qwen3-4B random-init
+    model's 8 GB took 7.8 s as ``model.to(device)``."""
+    from .staging import H2DStager
+    st = H2DStager(device)
     for m in model.modules():
         for store in (m._parameters, m._buffers):
             for name, t in list(store.items()):
                 if t is None or t.device.type != "cpu":
                     continue
-                src = t.detach().contiguous()
-                dst = torch.empty(src.shape, dtype=src.dtype, device=device)
-                sb, db = src.reshape(-1).view(torch.uint8), dst.reshape(-1).view(torch.uint8)
-                for off in range(0, sb.numel(), chunk_bytes):
-                    n = min(chunk_bytes, sb.numel() - off)
-                    i = k % 2
-                    if done[i] is not None:
-                        done[i].synchronize()  # the DMA that last read this staging buffer
-                    stage[i][:n].copy_(sb[off:off + n])
-                    with torch.cuda.stream(st):
-                        db[off:off + n].copy_(stage[i][:n], non_blocking=True)
-                        done[i] = torch.cuda.Event()
-                        done[i].record(st)
-                    k += 1
+                dst = st.copy(t)
                 if isinstance(t, nn.Parameter):
                     t.data = dst
                 else:

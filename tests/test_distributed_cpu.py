@@ -104,7 +104,7 @@ class _OraclePlan:
     save_compressed runs here; on GPUs the same logic drives the HIP kernels (tests/
     test_multirank_save_gpu.py)."""
 
-    def __init__(self, units, device):
+    def __init__(self, units, device, stager=None):
         import ct_torch as ct
         self.out = {}
         for u in units:

@@ -98,6 +98,26 @@ def test_rtn_w4a16_save_roundtrip(cuda, tmp_path):
     _eq(dec["model.layers.0.mlp.down_proj.weight"], ct.dequantize(q, s, None, oa, dtype=torch.bfloat16))
 
 
+def test_rtn_host_resident_model_staged(cuda, monkeypatch):
+    """A host-resident model (RTN recipe: oneshot moves nothing): save-time compression stages the
+    weights through the pinned buffers, in several plan chunks sharing one stager, and gives the
+    same tensors as the device-resident model and the oracle."""
+    import quantizers_amd.compressor as comp
+    recipe = {"s": {"m": {"QuantizationModifier": {"scheme": "W4A16", "targets": "Linear", "ignore": ["lm_head"]}}}}
+    m = _qwen3()
+    oneshot(m, recipe, device=cuda)
+    assert next(m.parameters()).device.type == "cpu"
+    monkeypatch.setattr(comp, "STAGE_BYTES", 300 << 10)  # several plans
+    host_sd = compressed_state_dict(m, cuda)
+    assert _check_against_oracle(m, host_sd) == 14
+    md = _qwen3().to(cuda)
+    oneshot(md, recipe)
+    dev_sd = compressed_state_dict(md)
+    assert set(host_sd) == set(dev_sd)
+    for k in host_sd:
+        _eq(host_sd[k], dev_sd[k], k)
+
+
 def test_documented_patch_keeps_quantization_config(cuda, tmp_path):
     """INTEGRATION.md's do_oneshot.py patch: save_compressed(model, dir) and then the
     reference's own model.config.save_pretrained(dir) (e.g. left in by a maintainer) -- the
