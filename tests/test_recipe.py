@@ -123,3 +123,25 @@ def test_run_config(tmp_path):
     bad.write_text("model: {name: x}\nquantization: {recipe: nope.yaml}\n")
     with pytest.raises(ValueError):
         load_run_config(str(bad)).resolve_recipe()
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference not mounted")
+def test_reference_run_configs_resolve():
+    """Every run config the reference ships (configs/*.yaml) loads with the reference's path rules:
+    recipe found and parsed, calibration-set file found and validated, output dir named as
+    do_oneshot.py:114-121 names it; the AutoRound config raises NotImplementedError (out of scope)."""
+    import glob
+    from quantizers_amd.config import load_run_config
+    files = sorted(glob.glob(os.path.join(os.path.dirname(REF), "*.yaml")))
+    assert len(files) >= 6
+    for f in files:
+        run = load_run_config(f)
+        assert run.calibration is not None, f
+        recipe = run.resolve_recipe()
+        if "-ar" in os.path.basename(f):
+            with pytest.raises(NotImplementedError):
+                parse_recipe(recipe)
+            continue
+        mods = parse_recipe(recipe)
+        assert mods and all(m.config_groups or getattr(m, "mappings", None) is not None for m in mods), f
+        assert run.output_dir().startswith("outputs/")
