@@ -117,9 +117,15 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
     mappings = awq.mappings or awq_mod.DEFAULT_MAPPINGS
     inputs = _capture_layer0_inputs(model, layers, batches)
     mtype = model_type(model)
+    stager = None
     for i, layer in enumerate(layers):
         home = next(layer.parameters()).device
-        layer.to(device)
+        host = None
+        if home != device:  # layer-by-layer onload: pinned staging, the host tensors kept for the offload
+            if stager is None:
+                from .staging import H2DStager
+                stager = H2DStager(device)
+            host = _onload(layer, stager)
         t0 = time.time()
         rep = awq_mod.awq_layer(layer, checkpoint_name(f"{lname}.{i}", mtype), inputs, mappings, weights,
                                 awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts,
@@ -130,8 +136,8 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
             out = _layer_out(layer(*args, **kwargs))
             nxt.append(((out,) + tuple(args[1:]), kwargs))
         inputs = nxt
-        if home != device:
-            layer.to(home)
+        if host is not None:
+            _offload(layer, host)
         log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), time.time() - t0)
 
 
@@ -205,6 +211,41 @@ def _to_device_staged(model: nn.Module, device) -> None:
                 else:
                     store[name] = dst
     st.synchronize()
+
+
+def _onload(module: nn.Module, stager) -> Dict[tuple, torch.Tensor]:
+    """Move ``module``'s host parameters / buffers to the stager's device; returns the host
+    tensors (by module, kind and name of their slot) so ``_offload`` can copy the results back into them."""
+    host: Dict[tuple, torch.Tensor] = {}
+    for m in module.modules():
+        for store in (m._parameters, m._buffers):
+            for name, t in list(store.items()):
+                if t is None or t.device.type != "cpu":
+                    continue
+                dst = stager.copy(t)
+                host[(id(m), store is m._buffers, name)] = t.data if isinstance(t, nn.Parameter) else t
+                if isinstance(t, nn.Parameter):
+                    t.data = dst
+                else:
+                    store[name] = dst
+    stager.wait()
+    return host
+
+
+def _offload(module: nn.Module, host: Dict) -> None:
+    """Copy the (smoothed) device tensors back into their original host tensors and point the
+    module at those again: the host pages are already resident, no new allocation."""
+    for m in module.modules():
+        for is_buf, store in ((False, m._parameters), (True, m._buffers)):
+            for name, t in list(store.items()):
+                h = host.get((id(m), is_buf, name))
+                if h is None:
+                    continue
+                h.copy_(t.detach())
+                if isinstance(t, nn.Parameter):
+                    t.data = h
+                else:
+                    store[name] = h
 
 
 def _fits_on_device(model: nn.Module, device) -> bool:
