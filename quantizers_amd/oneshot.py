@@ -175,7 +175,10 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             if device_resident if device_resident is not None else _fits_on_device(model, device):
                 # 288 GB of HBM: a model that fits moves to the device once and stays there (no
                 # per-layer onload / offload over PCIe; save_compressed then needs no staging)
+                t0 = time.time()
                 _to_device_staged(model, device)
+                log.info("model moved to %s in %.2fs (%.2f GB)", device, time.time() - t0,
+                         sum(p.numel() * p.element_size() for p in model.parameters()) / 1e9)
             else:
                 # embeddings / rotary / final norm run on the device; layers are onloaded one
                 # by one (the reference's sequential-pipeline placement)
