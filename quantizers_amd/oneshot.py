@@ -14,6 +14,7 @@ scheme of each targeted module (same names as the reference's per-expert Linear 
 from __future__ import annotations
 
 import logging
+import threading
 import time
 from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
 
@@ -203,17 +204,24 @@ def _to_device_staged(model: nn.Module, device) -> None:
     model's 8 GB took 7.8 s as ``model.to(device)``."""
     from .staging import H2DStager
     st = H2DStager(device)
+    old: List[torch.Tensor] = []  # host storage released only after the last DMA (see below)
     for m in model.modules():
         for store in (m._parameters, m._buffers):
             for name, t in list(store.items()):
                 if t is None or t.device.type != "cpu":
                     continue
                 dst = st.copy(t)
+                old.append(t.data if isinstance(t, nn.Parameter) else t)
                 if isinstance(t, nn.Parameter):
                     t.data = dst
                 else:
                     store[name] = dst
     st.synchronize()
+    # Unmapping host pages while DMAs run slows the DMAs ~6x on this platform (the Qwen3-4B move:
+    # copy phase 1.6-1.8 s freeing as it goes vs 0.27-0.29 s deferred, profiles/r02ad_stage_probe.log),
+    # and the unmapping itself takes ~0.6 s for 8 GB: it runs on a helper thread, beside the
+    # calibration work that follows.
+    threading.Thread(target=old.clear, name="qz-host-release", daemon=True).start()
 
 
 def _onload(module: nn.Module, stager) -> Dict[tuple, torch.Tensor]:

@@ -9,6 +9,8 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import time
+
 import torch
 
 
@@ -20,6 +22,7 @@ class H2DStager:
         self._stage: Optional[List[torch.Tensor]] = None
         self._done: List[Optional[torch.cuda.Event]] = [None, None]
         self._k = 0
+        self.stats = {"bytes": 0, "alloc_s": 0.0, "wait_s": 0.0, "memcpy_s": 0.0, "enqueue_s": 0.0}
 
     def _buffers(self) -> List[torch.Tensor]:
         if self._stage is None:
@@ -29,9 +32,12 @@ class H2DStager:
     def copy(self, src: torch.Tensor) -> torch.Tensor:
         """Enqueue the copy of host tensor ``src``; returns its (not yet filled) device tensor."""
         src = src.detach()
+        t0 = time.perf_counter()
         dst = torch.empty(src.shape, dtype=src.dtype, device=self.device)
+        self.stats["alloc_s"] += time.perf_counter() - t0
         if src.numel() == 0:
             return dst
+        self.stats["bytes"] += src.numel() * src.element_size()
         dst.record_stream(self.stream)  # not reused by the allocator before its DMA has run
         if src.is_pinned() and src.is_contiguous():  # DMA straight from the caller's pinned memory
             with torch.cuda.stream(self.stream):
@@ -47,13 +53,19 @@ class H2DStager:
         for off in range(0, sb.numel(), self.chunk):
             n = min(self.chunk, sb.numel() - off)
             i = self._k % 2
+            t0 = time.perf_counter()
             if self._done[i] is not None:
                 self._done[i].synchronize()  # the DMA that last read this staging buffer
+            t1 = time.perf_counter()
             stage[i][:n].copy_(sb[off:off + n])
+            t2 = time.perf_counter()
             with torch.cuda.stream(self.stream):
                 db[off:off + n].copy_(stage[i][:n], non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.stream)
+            self.stats["wait_s"] += t1 - t0
+            self.stats["memcpy_s"] += t2 - t1
+            self.stats["enqueue_s"] += time.perf_counter() - t2
             self._done[i] = ev
             self._k += 1
         return dst
