@@ -15,7 +15,9 @@ scripts/recombine_weights_MiniMax-M2.1.py:82-134.  MoE experts are written per e
 from __future__ import annotations
 
 import json
+import logging
 import os
+import time
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -25,6 +27,8 @@ from safetensors.torch import load_file, save_file
 from torch import nn
 
 from . import ops
+
+log = logging.getLogger(__name__)
 from .model import LinearRef, batch_groups, checkpoint_name, iter_linears, model_type, stacked_view
 from .quantization import QuantizationArgs, QuantizationScheme, compression_format
 
@@ -326,6 +330,7 @@ def _dist_info() -> Tuple[int, int]:
 
 
 STAGE_BYTES = 4 << 30  # host-resident weights staged on the device per plan
+WRITE_THREADS = int(os.environ.get("QZ_WRITE_THREADS", "4"))  # concurrent shard-file writers
 
 
 @torch.no_grad()
@@ -388,13 +393,17 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
     ``torch.distributed`` the compression is sharded over the ranks (``compressed_state_dict``)
     and rank 0 alone writes; every rank returns after the files exist."""
     world, rank = _dist_info()
+    t0 = time.perf_counter()
     sd = compressed_state_dict(model, device, dst=0)
+    t1 = time.perf_counter()
     qcfg = quantization_config(model)
     if hasattr(model, "config"):
         # so a later model.config.save_pretrained(output_dir) keeps the compressed-tensors config
         model.config.quantization_config = qcfg
     if rank == 0:
         _write_checkpoint(sd, model, qcfg, output_dir, max_shard_bytes)
+        log.info("save_compressed: %d tensors, %.2f GB; compress + device->host %.2fs, write %.2fs", len(sd),
+                 sum(t.numel() * t.element_size() for t in sd.values()) / 1e9, t1 - t0, time.perf_counter() - t1)
     if world > 1:
         dist.barrier()
     return output_dir
@@ -419,9 +428,14 @@ def _write_checkpoint(sd: Dict[str, torch.Tensor], model: nn.Module, qcfg: dict,
     else:
         wmap = {}
         total = 0
-        for i, sh in enumerate(shards):
-            fn = f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors"
-            save_file(sh, os.path.join(output_dir, fn), metadata=meta)
+        fns = [f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors" for i in range(len(shards))]
+        # shard files written concurrently (WRITE_THREADS; 1 = one after the other)
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=max(1, min(WRITE_THREADS, len(shards)))) as pool:
+            for f in [pool.submit(save_file, sh, os.path.join(output_dir, fn), metadata=meta)
+                      for sh, fn in zip(shards, fns)]:
+                f.result()
+        for sh, fn in zip(shards, fns):
             for n, t in sh.items():
                 wmap[n] = fn
                 total += t.numel() * t.element_size()
