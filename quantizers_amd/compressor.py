@@ -86,6 +86,11 @@ class CompressUnit:
         w = stacked_view(self.refs)
         return w if self.stacked else w[0]
 
+    def base(self) -> Optional[torch.Tensor]:
+        """The fused parameter a stacked / expert unit is a view of (None for a dense Linear)."""
+        r0 = self.refs[0]
+        return getattr(r0.module, r0.param_name).data if r0.index is not None else None
+
     @property
     def nbytes(self) -> int:
         return sum(r.weight.numel() for r in self.refs) * 2
@@ -154,6 +159,7 @@ class CompressionPlan:
         buckets: Dict[tuple, list] = {}
         self.params = 0
         staged = False
+        bases: Dict[int, torch.Tensor] = {}  # host fused parameter -> its staged device copy
         for u in units:
             a = u.scheme.weights
             w = u.view()
@@ -161,7 +167,18 @@ class CompressionPlan:
                 if stager is None:
                     from .staging import H2DStager
                     stager = H2DStager(self.device)
-                w = stager.copy(w)
+                base = u.base()
+                if base is not None and not w.is_contiguous() and base.is_contiguous() \
+                        and w.untyped_storage().data_ptr() == base.untyped_storage().data_ptr():
+                    # a strided slice of a fused expert parameter (gate / up halves): stage the
+                    # parameter once, contiguously, and take the same view on the device -- no
+                    # host-side gather copy (58 GB of them cost 7 s on Qwen3-30B-A3B)
+                    key = base.data_ptr()
+                    if key not in bases:
+                        bases[key] = stager.copy(base)
+                    w = bases[key].as_strided(w.size(), w.stride(), w.storage_offset() - base.storage_offset())
+                else:
+                    w = stager.copy(w)
                 staged = True
             self.params += w.numel()
             int_q, fmt = ops._compress_plan(a, u.scheme.input_activations is not None)
@@ -359,14 +376,27 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
     if device.type == "cuda" and any(u.refs[0].weight.device != device for u in mine):
         from .staging import H2DStager
         stager = H2DStager(device)  # one pair of pinned buffers for every chunk
+    tm = {"plan": 0.0, "run": 0.0, "tensors": 0.0, "submit": 0.0, "finish": 0.0}
     for chunk in _chunks(mine, STAGE_BYTES, device):
+        t0 = time.perf_counter()
         plan = CompressionPlan(chunk, device, stager)
+        t1 = time.perf_counter()
         plan.run()
+        t2 = time.perf_counter()
         t = plan.tensors()
+        t3 = time.perf_counter()
         local.update(copier.submit(t) if copier is not None else t)
+        tm["plan"] += t1 - t0
+        tm["run"] += t2 - t1
+        tm["tensors"] += t3 - t2
+        tm["submit"] += time.perf_counter() - t3
         del plan
+    t0 = time.perf_counter()
     if copier is not None:
         copier.finish()
+    tm["finish"] = time.perf_counter() - t0
+    log.info("compressed_state_dict phases (s): %s%s", {k: round(v, 3) for k, v in tm.items()},
+             f" staging {stager.stats}" if stager is not None else "")
     receiver = world == 1 or dst is None or rank == dst
     if world > 1:
         from .distributed import gather_state
@@ -380,9 +410,14 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
             copier = _HostCopier(device)
             out.update(copier.submit(dev_raw))
             copier.finish()
-        for k, v in raw.items():
-            if not v.is_cuda:
-                out[k] = v.clone()
+        # host tensors are written as they are (no copy), except those sharing storage with
+        # another output (tied embeddings): safetensors refuses shared storage
+        host_raw = {k: v for k, v in raw.items() if not v.is_cuda}
+        users: Dict[int, int] = {}
+        for v in host_raw.values():
+            users[v.untyped_storage().data_ptr()] = users.get(v.untyped_storage().data_ptr(), 0) + 1
+        for k, v in host_raw.items():
+            out[k] = v.clone() if users[v.untyped_storage().data_ptr()] > 1 else v
     else:
         out.update(raw)
     return out

@@ -98,19 +98,26 @@ def test_rtn_w4a16_save_roundtrip(cuda, tmp_path):
     _eq(dec["model.layers.0.mlp.down_proj.weight"], ct.dequantize(q, s, None, oa, dtype=torch.bfloat16))
 
 
-def test_rtn_host_resident_model_staged(cuda, monkeypatch):
+@pytest.mark.parametrize("moe", [False, True], ids=["dense", "moe"])
+def test_rtn_host_resident_model_staged(cuda, monkeypatch, moe):
     """A host-resident model (RTN recipe: oneshot moves nothing): save-time compression stages the
-    weights through the pinned buffers, in several plan chunks sharing one stager, and gives the
-    same tensors as the device-resident model and the oracle."""
+    weights through the pinned buffers, in several plan chunks sharing one stager (fused expert
+    parameters staged whole and sliced on the device), and gives the same tensors as the
+    device-resident model and the oracle."""
     import quantizers_amd.compressor as comp
+    build = _qwen3_moe if moe else _qwen3
     recipe = {"s": {"m": {"QuantizationModifier": {"scheme": "W4A16", "targets": "Linear", "ignore": ["lm_head"]}}}}
-    m = _qwen3()
+    if moe:  # int4 g32 on the experts only (the other linears stay bf16)
+        recipe = {"s": {"m": {"QuantizationModifier": {"config_groups": {"g": {
+            "targets": ["re:.*mlp\\.experts\\.\\d+\\.(down_proj|gate_proj|up_proj)$"],
+            "weights": {"num_bits": 4, "type": "int", "symmetric": True, "strategy": "group", "group_size": 32}}}}}}}
+    m = build()
     oneshot(m, recipe, device=cuda)
     assert next(m.parameters()).device.type == "cpu"
     monkeypatch.setattr(comp, "STAGE_BYTES", 300 << 10)  # several plans
     host_sd = compressed_state_dict(m, cuda)
-    assert _check_against_oracle(m, host_sd) == 14
-    md = _qwen3().to(cuda)
+    assert _check_against_oracle(m, host_sd) == (2 * 8 * 3 if moe else 14)
+    md = build().to(cuda)
     oneshot(md, recipe)
     dev_sd = compressed_state_dict(md)
     assert set(host_sd) == set(dev_sd)
