@@ -299,6 +299,10 @@ class _HostCopier:
         self.budget = budget
 
     def submit(self, items: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Enqueue the device -> host copies of ``items``; returns host tensors (valid once
+        ``last_event`` completes).  Tensors that are views of one device storage (the per-expert
+        slices of a stacked output) travel as ONE copy of that storage, and their host views are
+        cut from its pinned copy: a few large DMAs instead of one per tensor."""
         dev_items = {k: t for k, t in items.items() if t.is_cuda}
         host = {k: t for k, t in items.items() if not t.is_cuda}
         if not dev_items:
@@ -306,17 +310,22 @@ class _HostCopier:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ready)
-        offs, total = {}, 0
-        for k, t in dev_items.items():
-            offs[k] = total
-            total += (t.numel() * t.element_size() + 63) // 64 * 64
+        stores: Dict[int, Tuple[torch.UntypedStorage, int]] = {}  # storage ptr -> (storage, buffer offset)
+        total = 0
+        for t in dev_items.values():
+            st = t.untyped_storage()
+            if st.data_ptr() not in stores:
+                stores[st.data_ptr()] = (st, total)
+                total += (st.nbytes() + 63) // 64 * 64
         buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=True)
         with torch.cuda.stream(self.stream):
-            for k, t in dev_items.items():
-                nb = t.numel() * t.element_size()
-                h = buf[offs[k]:offs[k] + nb].view(t.dtype).view(t.shape)
-                h.copy_(t.contiguous(), non_blocking=True)
-                host[k] = h
+            for st, off in stores.values():
+                src = torch.empty(0, dtype=torch.uint8, device=self.device).set_(st, 0, (st.nbytes(),), (1,))
+                buf[off:off + st.nbytes()].copy_(src, non_blocking=True)
+        for k, t in dev_items.items():
+            st, off = stores[t.untyped_storage().data_ptr()]
+            flat = buf[off:off + st.nbytes()].view(t.dtype)
+            host[k] = flat.as_strided(t.size(), t.stride(), flat.storage_offset() + t.storage_offset())
         done = torch.cuda.Event()
         done.record(self.stream)
         self.pending.append((done, list(dev_items.values()), total))
