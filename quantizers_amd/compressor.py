@@ -359,6 +359,55 @@ STAGE_BYTES = 4 << 30  # host-resident weights staged on the device per plan
 WRITE_THREADS = int(os.environ.get("QZ_WRITE_THREADS", "4"))  # concurrent shard-file writers
 
 
+def _compress_chunks(units: Sequence[CompressUnit], device, copier: Optional["_HostCopier"], timings: Dict[str, float]):
+    """Compress ``units`` plan by plan (at most STAGE_BYTES of host weights staged per plan);
+    yields each plan's on-disk tensors -- pinned-host views when ``copier`` is given (valid once
+    ``copier.last_event`` completes), device tensors otherwise."""
+    stager = None
+    if device.type == "cuda" and any(u.refs[0].weight.device != device for u in units):
+        from .staging import H2DStager
+        stager = H2DStager(device)  # one pair of pinned buffers for every chunk
+    for k in ("plan", "run", "tensors", "submit"):
+        timings.setdefault(k, 0.0)
+    for chunk in _chunks(units, STAGE_BYTES, device):
+        t0 = time.perf_counter()
+        plan = CompressionPlan(chunk, device, stager)
+        t1 = time.perf_counter()
+        plan.run()
+        t2 = time.perf_counter()
+        t = plan.tensors()
+        t3 = time.perf_counter()
+        out = copier.submit(t) if copier is not None else t
+        timings["plan"] += t1 - t0
+        timings["run"] += t2 - t1
+        timings["tensors"] += t3 - t2
+        timings["submit"] += time.perf_counter() - t3
+        del plan
+        yield out
+    if stager is not None:
+        timings["staging"] = dict(stager.stats)
+
+
+def _raw_to_host(raw: Dict[str, torch.Tensor], device,
+                 copier: Optional["_HostCopier"] = None) -> Tuple[Dict[str, torch.Tensor], Optional["_HostCopier"]]:
+    """The unchanged tensors on the host: device ones through a pinned copier (``copier``, or a
+    new one; returned, to be finished by the caller), host ones as they are -- except those
+    sharing storage with another output (tied embeddings), cloned because safetensors refuses
+    shared storage."""
+    out: Dict[str, torch.Tensor] = {}
+    dev_raw = {k: v for k, v in raw.items() if v.is_cuda}
+    if dev_raw:
+        copier = copier if copier is not None else _HostCopier(device)
+        out.update(copier.submit(dev_raw))
+    host_raw = {k: v for k, v in raw.items() if not v.is_cuda}
+    users: Dict[int, int] = {}
+    for v in host_raw.values():
+        users[v.untyped_storage().data_ptr()] = users.get(v.untyped_storage().data_ptr(), 0) + 1
+    for k, v in host_raw.items():
+        out[k] = v.clone() if users[v.untyped_storage().data_ptr()] > 1 else v
+    return out, copier
+
+
 @torch.no_grad()
 def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
                           dst: Optional[int] = None) -> Dict[str, torch.Tensor]:
@@ -381,31 +430,12 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
         mine = [u for i, u in enumerate(units) if i in keep]
     copier = _HostCopier(device) if (to_host and world == 1 and device.type == "cuda") else None
     local: Dict[str, torch.Tensor] = {}
-    stager = None
-    if device.type == "cuda" and any(u.refs[0].weight.device != device for u in mine):
-        from .staging import H2DStager
-        stager = H2DStager(device)  # one pair of pinned buffers for every chunk
-    tm = {"plan": 0.0, "run": 0.0, "tensors": 0.0, "submit": 0.0, "finish": 0.0}
-    for chunk in _chunks(mine, STAGE_BYTES, device):
-        t0 = time.perf_counter()
-        plan = CompressionPlan(chunk, device, stager)
-        t1 = time.perf_counter()
-        plan.run()
-        t2 = time.perf_counter()
-        t = plan.tensors()
-        t3 = time.perf_counter()
-        local.update(copier.submit(t) if copier is not None else t)
-        tm["plan"] += t1 - t0
-        tm["run"] += t2 - t1
-        tm["tensors"] += t3 - t2
-        tm["submit"] += time.perf_counter() - t3
-        del plan
-    t0 = time.perf_counter()
+    tm: Dict[str, float] = {}
+    for t in _compress_chunks(mine, device, copier, tm):
+        local.update(t)
     if copier is not None:
         copier.finish()
-    tm["finish"] = time.perf_counter() - t0
-    log.info("compressed_state_dict phases (s): %s%s", {k: round(v, 3) for k, v in tm.items()},
-             f" staging {stager.stats}" if stager is not None else "")
+    log.info("compressed_state_dict phases (s): %s", tm)
     receiver = world == 1 or dst is None or rank == dst
     if world > 1:
         from .distributed import gather_state
@@ -413,78 +443,135 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
     if not receiver:
         return {}
     out = dict(local)
-    dev_raw = {k: v for k, v in raw.items() if v.is_cuda}
     if to_host:
-        if dev_raw:
-            copier = _HostCopier(device)
-            out.update(copier.submit(dev_raw))
-            copier.finish()
-        # host tensors are written as they are (no copy), except those sharing storage with
-        # another output (tied embeddings): safetensors refuses shared storage
-        host_raw = {k: v for k, v in raw.items() if not v.is_cuda}
-        users: Dict[int, int] = {}
-        for v in host_raw.values():
-            users[v.untyped_storage().data_ptr()] = users.get(v.untyped_storage().data_ptr(), 0) + 1
-        for k, v in host_raw.items():
-            out[k] = v.clone() if users[v.untyped_storage().data_ptr()] > 1 else v
+        host_raw, rc = _raw_to_host(raw, device)
+        out.update(host_raw)
+        if rc is not None:
+            rc.finish()
     else:
         out.update(raw)
     return out
 
 
+def _order_key(units: Sequence[CompressUnit], raw: Dict[str, torch.Tensor]):
+    """Checkpoint tensor order (and so the shard split): compression units in model order, names
+    sorted within a unit, then the unchanged tensors by name -- the same whether the tensors come
+    from one process chunk by chunk or from the ranks' all-gather."""
+    unit_of = {r.name: i for i, u in enumerate(units) for r in u.refs}
+    last = len(units)
+
+    def key(name: str):
+        if name in raw:
+            return (last, name)
+        return (unit_of.get(name.rsplit(".", 1)[0], last), name)
+    return key
+
+
 def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SHARD_BYTES, device=None) -> str:
-    """Write safetensors shards + index + config.json(quantization_config).  Under
-    ``torch.distributed`` the compression is sharded over the ranks (``compressed_state_dict``)
-    and rank 0 alone writes; every rank returns after the files exist."""
+    """Write safetensors shards + index + config.json(quantization_config).  One process: the
+    shards stream out while the next plans compress (a shard is handed to a writer thread as
+    soon as its bytes are on the host).  Under ``torch.distributed`` the compression is sharded
+    over the ranks (``compressed_state_dict``) and rank 0 alone writes; every rank returns after
+    the files exist."""
     world, rank = _dist_info()
-    t0 = time.perf_counter()
-    sd = compressed_state_dict(model, device, dst=0)
-    t1 = time.perf_counter()
+    device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     qcfg = quantization_config(model)
     if hasattr(model, "config"):
         # so a later model.config.save_pretrained(output_dir) keeps the compressed-tensors config
         model.config.quantization_config = qcfg
+    t0 = time.perf_counter()
+    units, raw = compression_units(model)
+    key = _order_key(units, raw)
+    n_tensors, n_bytes = 0, 0
+    if world == 1 and device.type == "cuda":
+        writer = _ShardWriter(output_dir, max_shard_bytes)
+        copier = _HostCopier(device)
+        tm: Dict[str, float] = {}
+        for t in _compress_chunks(units, device, copier, tm):
+            writer.add(sorted(t.items(), key=lambda kv: key(kv[0])), copier.last_event)
+        host_raw, _ = _raw_to_host(raw, device, copier)  # same copier stream: its last event covers all
+        writer.add(sorted(host_raw.items()), copier.last_event)
+        n_tensors, n_bytes = writer.close()
+        copier.finish()
+        log.info("compressed_state_dict phases (s): %s", tm)
+    else:
+        sd = compressed_state_dict(model, device, dst=0)
+        if rank == 0:
+            writer = _ShardWriter(output_dir, max_shard_bytes)
+            writer.add(sorted(sd.items(), key=lambda kv: key(kv[0])))
+            n_tensors, n_bytes = writer.close()
     if rank == 0:
-        _write_checkpoint(sd, model, qcfg, output_dir, max_shard_bytes)
-        log.info("save_compressed: %d tensors, %.2f GB; compress + device->host %.2fs, write %.2fs", len(sd),
-                 sum(t.numel() * t.element_size() for t in sd.values()) / 1e9, t1 - t0, time.perf_counter() - t1)
+        _write_config(model, qcfg, output_dir)
+        log.info("save_compressed: %d tensors, %.2f GB in %.2fs", n_tensors, n_bytes / 1e9, time.perf_counter() - t0)
     if world > 1:
         dist.barrier()
     return output_dir
 
 
-def _write_checkpoint(sd: Dict[str, torch.Tensor], model: nn.Module, qcfg: dict, output_dir: str,
-                      max_shard_bytes: int) -> None:
-    os.makedirs(output_dir, exist_ok=True)
-    names = sorted(sd)
-    shards: List[Dict[str, torch.Tensor]] = [{}]
-    size = 0
-    for n in names:
-        nb = sd[n].numel() * sd[n].element_size()
-        if shards[-1] and size + nb > max_shard_bytes:
-            shards.append({})
-            size = 0
-        shards[-1][n] = sd[n].contiguous()
-        size += nb
-    meta = {"format": "pt"}
-    if len(shards) == 1:
-        save_file(shards[0], os.path.join(output_dir, "model.safetensors"), metadata=meta)
-    else:
-        wmap = {}
-        total = 0
-        fns = [f"model-{i + 1:05d}-of-{len(shards):05d}.safetensors" for i in range(len(shards))]
-        # shard files written concurrently (WRITE_THREADS; 1 = one after the other)
+def _write_shard_file(shard: Dict[str, torch.Tensor], path: str, ready) -> None:
+    if ready is not None:
+        ready.synchronize()  # the shard's device -> host copies have landed
+    save_file({k: v.contiguous() for k, v in shard.items()}, path, metadata={"format": "pt"})
+
+
+class _ShardWriter:
+    """safetensors shards of at most ``max_shard_bytes`` in the order tensors are added, each
+    written by a pool thread (WRITE_THREADS) once complete; ``close`` names them
+    ``model.safetensors`` (one shard) or ``model-XXXXX-of-NNNNN.safetensors`` + index."""
+
+    def __init__(self, output_dir: str, max_shard_bytes: int):
         from concurrent.futures import ThreadPoolExecutor
-        with ThreadPoolExecutor(max_workers=max(1, min(WRITE_THREADS, len(shards)))) as pool:
-            for f in [pool.submit(save_file, sh, os.path.join(output_dir, fn), metadata=meta)
-                      for sh, fn in zip(shards, fns)]:
+        os.makedirs(output_dir, exist_ok=True)
+        self.dir, self.max = output_dir, max_shard_bytes
+        self.cur: Dict[str, torch.Tensor] = {}
+        self.size = 0
+        self.ready = None
+        self.shards: List[Tuple[str, Dict[str, int]]] = []
+        self.pool = ThreadPoolExecutor(max_workers=max(1, WRITE_THREADS))
+        self.futures = []
+
+    def add(self, items, ready=None) -> None:
+        if ready is not None:
+            self.ready = ready  # one stream: the latest copy event covers every earlier copy
+        for n, t in items:
+            nb = t.numel() * t.element_size()
+            if self.cur and self.size + nb > self.max:
+                self._flush()
+            self.cur[n] = t
+            self.size += nb
+
+    def _flush(self) -> None:
+        path = os.path.join(self.dir, f".qz-shard-{len(self.shards):05d}.tmp")
+        self.shards.append((path, {n: t.numel() * t.element_size() for n, t in self.cur.items()}))
+        self.futures.append(self.pool.submit(_write_shard_file, self.cur, path, self.ready))
+        self.cur, self.size = {}, 0
+
+    def close(self) -> Tuple[int, int]:
+        if self.cur or not self.shards:
+            self._flush()
+        try:
+            for f in self.futures:
                 f.result()
-        for sh, fn in zip(shards, fns):
-            for n, t in sh.items():
-                wmap[n] = fn
-                total += t.numel() * t.element_size()
-        with open(os.path.join(output_dir, "model.safetensors.index.json"), "w") as f:
-            json.dump({"metadata": {"total_size": total}, "weight_map": wmap}, f, indent=2)
+        finally:
+            self.pool.shutdown()
+        n = len(self.shards)
+        total = sum(nb for _, names in self.shards for nb in names.values())
+        count = sum(len(names) for _, names in self.shards)
+        if n == 1:
+            os.replace(self.shards[0][0], os.path.join(self.dir, "model.safetensors"))
+            return count, total
+        wmap = {}
+        for i, (path, names) in enumerate(self.shards):
+            fn = f"model-{i + 1:05d}-of-{n:05d}.safetensors"
+            os.replace(path, os.path.join(self.dir, fn))
+            for nm in names:
+                wmap[nm] = fn
+        with open(os.path.join(self.dir, "model.safetensors.index.json"), "w") as f:
+            json.dump({"metadata": {"total_size": total}, "weight_map": dict(sorted(wmap.items()))}, f, indent=2)
+        return count, total
+
+
+def _write_config(model: nn.Module, qcfg: dict, output_dir: str) -> None:
     cfg = model.config.to_dict() if hasattr(model, "config") else {}
     cfg["quantization_config"] = qcfg
     with open(os.path.join(output_dir, "config.json"), "w") as f:

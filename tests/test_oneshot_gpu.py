@@ -125,6 +125,34 @@ def test_rtn_host_resident_model_staged(cuda, monkeypatch, moe):
         _eq(host_sd[k], dev_sd[k], k)
 
 
+@pytest.mark.parametrize("resident", [True, False], ids=["device", "host"])
+def test_streamed_shards_match_state_dict(cuda, tmp_path, resident):
+    """save_compressed streams shards while it compresses: with a small shard size the files
+    (model-XXXXX-of-NNNNN + index) hold exactly compressed_state_dict's tensors, in unit order,
+    and no temporary file is left."""
+    from safetensors.torch import load_file
+    recipe = {"s": {"m": {"QuantizationModifier": {"scheme": "W4A16", "targets": "Linear", "ignore": ["lm_head"]}}}}
+    m = _qwen3()
+    if resident:
+        m = m.to(cuda)
+    oneshot(m, recipe, device=cuda)
+    out = save_compressed(m, str(tmp_path / "ck"), max_shard_bytes=200 << 10, device=cuda)
+    files = sorted(os.listdir(out))
+    shards = [f for f in files if f.endswith(".safetensors")]
+    assert len(shards) > 3 and not any(f.endswith(".tmp") for f in files)
+    assert all(f.endswith(f"-of-{len(shards):05d}.safetensors") for f in shards)
+    idx = json.load(open(os.path.join(out, "model.safetensors.index.json")))
+    got = {}
+    for f in shards:
+        part = load_file(os.path.join(out, f))
+        assert all(idx["weight_map"][k] == f for k in part)
+        got.update(part)
+    want = compressed_state_dict(m, cuda)
+    assert set(got) == set(want) == set(idx["weight_map"])
+    for k in want:
+        _eq(got[k], want[k], k)
+
+
 def test_documented_patch_keeps_quantization_config(cuda, tmp_path):
     """INTEGRATION.md's do_oneshot.py patch: save_compressed(model, dir) and then the
     reference's own model.config.save_pretrained(dir) (e.g. left in by a maintainer) -- the
