@@ -215,6 +215,43 @@ def test_awq_int4_g32_end_to_end(cuda, tmp_path):
     assert open(os.path.join(out, "recipe.yaml")).read() == open(recipe).read()
 
 
+@pytest.mark.parametrize("arch", ["qwen2", "llama"])
+def test_awq_mha_with_biases(cuda, arch):
+    """Other llama-family decoders: full multi-head attention (so the v_proj -> o_proj mapping
+    runs: four mappings per layer) with q/k/v biases set to non-zero values.  Smoothing v_proj
+    must divide its bias too, or the smoothed model's output moves by W_o (s - 1) b; the check is
+    that smoothing preserves the function, and the checkpoint matches the oracle."""
+    from transformers import AutoModelForCausalLM, LlamaConfig, Qwen2Config
+    kw = dict(hidden_size=256, intermediate_size=512, num_hidden_layers=2, num_attention_heads=4,
+              num_key_value_heads=4, vocab_size=512, max_position_embeddings=256)
+    cfg = Qwen2Config(**kw) if arch == "qwen2" else LlamaConfig(attention_bias=True, **kw)
+    torch.manual_seed(0)
+    m = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("layernorm.weight"):
+                p.copy_((torch.rand_like(p.float()) * 1.5 + 0.25).to(p.dtype))
+            elif n.endswith(".bias"):
+                p.copy_((torch.rand_like(p.float()) - 0.5).to(p.dtype))
+    m = m.to(cuda)
+    calib = _calib()
+    ids = torch.stack([c["input_ids"] for c in calib]).to(cuda)
+    with torch.no_grad():
+        ref_logits = m(ids).logits.float()
+    v_bias0 = m.model.layers[0].self_attn.v_proj.bias.detach().clone()
+    oneshot(m, os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g32.yaml"), dataset=calib, max_seq_length=64)
+    for layer, maps in m.awq_report.items():
+        assert len(maps) == 4, maps.keys()  # v_proj -> o_proj included (no GQA)
+    assert not torch.equal(m.model.layers[0].self_attn.v_proj.bias, v_bias0)  # the bias was rescaled
+    with torch.no_grad():
+        new_logits = m(ids).logits.float()
+    rel = (new_logits - ref_logits).norm() / ref_logits.norm()
+    assert rel < 0.05, rel
+    sd = compressed_state_dict(m)
+    assert _check_against_oracle(m, sd) == 14
+    assert "model.layers.0.self_attn.v_proj.bias" in sd
+
+
 def test_awq_layer_matches_oracle_search(cuda):
     """Layer-0 AWQ: statistics, w_mean and grid losses from the GPU path vs a CPU restatement."""
     from quantizers_amd.quantization import QuantizationArgs
