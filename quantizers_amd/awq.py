@@ -37,6 +37,7 @@ per mapping).
 from __future__ import annotations
 
 import logging
+import os
 import re
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
@@ -197,6 +198,7 @@ class _ExpertInputs:
         self.x: List[torch.Tensor] = []
         self.topk: List[Optional[torch.Tensor]] = []
         self.gate_up0: Optional[torch.Tensor] = None  # pre-smoothing snapshot
+        self._xcat: Optional[torch.Tensor] = None  # every batch's tokens, concatenated (lazily)
         self.h = module.register_forward_pre_hook(self._hook)
 
     def _hook(self, mod, args):
@@ -220,6 +222,22 @@ class _ExpertInputs:
         """act(x W_gate^T) * (x W_up^T) for expert e: the input of its down projection."""
         gate, up = nn.functional.linear(self.tokens(i, e), self.gate_up0[e]).chunk(2, dim=-1)
         return self.module.act_fn(gate) * up
+
+    def hidden_cat(self, e: int) -> torch.Tensor:
+        """``cat([hidden(i, e) for every batch i])`` as ONE GEMM over the concatenated tokens:
+        hipBLASLt gives every row the same bits either way at these shapes
+        (``scripts/concat_probe.py``), and a 128-expert layer issues 128 GEMMs instead of 2,048."""
+        if self.calibrate_all or any(t is None for t in self.topk):
+            if self._xcat is None:
+                self._xcat = torch.cat(self.x) if len(self.x) > 1 else self.x[0]
+            x = self._xcat
+        else:
+            x = torch.cat([self.tokens(i, e) for i in range(len(self.x))])
+        gate, up = nn.functional.linear(x, self.gate_up0[e]).chunk(2, dim=-1)
+        return self.module.act_fn(gate) * up
+
+
+CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 
 
 def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
@@ -651,7 +669,10 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         a = quantized[chunk[0].balance_names[0]]
         es = [ref.index[0] for ref in refs]
         w2 = getattr(mod, pname).data  # [E, H, I]
-        hid = [[_virtual_input(ei, ref, i) for i in range(n_batches)] for ref in refs]  # [e][i] -> [T_i, I]
+        if CONCAT_EXPERT_INPUTS and all(r.param_name in ("down_proj", "w2") for r in refs):
+            hid = [[ei.hidden_cat(ref.index[0])] for ref in refs]  # [e] -> [[T, I]]
+        else:
+            hid = [[_virtual_input(ei, ref, i) for i in range(n_batches)] for ref in refs]  # [e][i] -> [T_i, I]
         cols = w2.shape[2]
         xm = torch.empty(len(refs), cols, dtype=torch.float32, device=w2.device)
         wm = torch.empty_like(xm)
