@@ -477,6 +477,33 @@ def _minimax(layers=2, experts=8):
     return m
 
 
+@pytest.mark.parametrize("arch", ["qwen3_moe", "minimax"])
+def test_moe_routed_experts_replay_is_bit_identical(cuda, monkeypatch, arch):
+    """AWQ grids whose parent is the MoE block replay the fixed routing without host syncs
+    (awq._RoutedExpertsReplay): every loss history and every smoothed parameter is bit-identical
+    to running the module's own experts forward."""
+    import quantizers_amd.awq as awq_mod
+    recipe = os.path.join(ROOT, "configs", "recipes",
+                          "awq_w4a16_g32.yaml" if arch == "qwen3_moe" else "minimax_awq_mixedprec.yaml")
+    out = {}
+    for replay in (True, False):
+        monkeypatch.setattr(awq_mod, "REPLAY_ROUTED_EXPERTS", replay)
+        m = (_qwen3_moe() if arch == "qwen3_moe" else _minimax()).to(cuda)
+        calib = _calib(vocab=256)
+        oneshot(m, recipe, dataset=calib, max_seq_length=64)
+        out[replay] = (m.awq_report, {n: p.detach().clone() for n, p in m.named_parameters()})
+    (rep1, p1), (rep0, p0) = out[True], out[False]
+    assert rep1.keys() == rep0.keys()
+    n_moe = 0
+    for layer in rep1:
+        for smooth, r in rep1[layer].items():
+            assert r.get("history") == rep0[layer][smooth].get("history"), (layer, smooth)
+            n_moe += "layernorm" in smooth and "post_attention" in smooth
+    assert n_moe >= 2  # the MoE-block-parent mappings ran (once per layer)
+    for n in p1:
+        _eq(p1[n], p0[n], n)
+
+
 def test_minimax_awq_mixedprec_end_to_end(cuda, tmp_path):
     """recipe_Minimax-M2.1-AWQ-MixedPrec semantics on a tiny random MiniMax-M2: FP8 g32 attention,
     int4 g32 experts, AWQ over attention, all experts' w1/w3 and each expert's w3 -> w2."""
