@@ -306,10 +306,13 @@ class _RoutedExpertsReplay:
             self.plans[key] = (top_k_index.clone(), plan)
             want = type(self.m).forward(self.m, hidden_states, top_k_index, top_k_weights)
             got = self._replay(hidden_states, top_k_weights, plan)
-            if not torch.equal(got.view(torch.int16) if got.dtype == torch.bfloat16 else got,
-                               want.view(torch.int16) if want.dtype == torch.bfloat16 else want):
-                log.info("AWQ: routed-experts replay differs from %s.forward; using the module's own",
-                         type(self.m).__name__)
+            if not _bits_equal(got, want):
+                again = type(self.m).forward(self.m, hidden_states, top_k_index, top_k_weights)
+                log.info("AWQ: routed-experts replay differs from %s.forward in %d of %d elements (max |d| %.3g; "
+                         "the module's forward run twice %s); using the module's own",
+                         type(self.m).__name__, int((got != want).sum()), want.numel(),
+                         float((got.float() - want.float()).abs().max()),
+                         "agrees with itself" if _bits_equal(again, want) else "DISAGREES with itself")
                 self.ok = False
             return want
         idx0, plan = self.plans[key]
@@ -321,6 +324,14 @@ class _RoutedExpertsReplay:
     def close(self) -> None:
         if self.changed is not None and bool(self.changed):
             raise RuntimeError("AWQ: the MoE routing changed inside a grid search (replay invalid)")
+
+
+def _bits_equal(a: torch.Tensor, b: torch.Tensor) -> bool:
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.dtype in (torch.bfloat16, torch.float16):
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a, b)
 
 
 class _ReplayExperts:
