@@ -13,6 +13,7 @@ scheme of each targeted module (same names as the reference's per-expert Linear 
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import threading
 import time
@@ -184,9 +185,10 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                 # embeddings / rotary / final norm run on the device; layers are onloaded one
                 # by one (the reference's sequential-pipeline placement)
                 _to_device_except(model, decoder_layers(model), device)
-        for m in awqs:
-            _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
-                            stateful_observers)
+        with _eager_experts(model):
+            for m in awqs:
+                _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
+                                stateful_observers)
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
     model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml
@@ -257,6 +259,30 @@ def _offload(module: nn.Module, host: Dict) -> None:
                     t.data = h
                 else:
                     store[name] = h
+
+
+@contextlib.contextmanager
+def _eager_experts(model: nn.Module):
+    """Run transformers' fused MoE experts in their eager form (per routed expert: GEMMs, routing
+    weight, bf16 ``index_add_`` in expert order) for the duration of the AWQ pass (decision D15).
+    The reference pins transformers 4.57, whose MoE blocks loop over per-expert Linear modules
+    exactly so; transformers 5's default ``grouped_mm`` form sums the top-k contributions in f32
+    instead, which would move every MoE-parent loss and propagated activation off the
+    reference's arithmetic.  In the eager form an AWQ grid with a MoE-block parent also replays
+    its fixed routing without host syncs (awq._RoutedExpertsReplay)."""
+    cfgs = {}
+    for mod in model.modules():
+        c = getattr(mod, "config", None)
+        if c is not None and hasattr(c, "_experts_implementation") and c._experts_implementation not in (None, "eager"):
+            cfgs[id(c)] = c
+    old = {k: c._experts_implementation for k, c in cfgs.items()}
+    try:
+        for c in cfgs.values():
+            c._experts_implementation = "eager"
+        yield
+    finally:
+        for k, c in cfgs.items():
+            c._experts_implementation = old[k]
 
 
 def _fits_on_device(model: nn.Module, device) -> bool:
