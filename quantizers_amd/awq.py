@@ -240,6 +240,7 @@ class _ExpertInputs:
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 REPLAY_ROUTED_EXPERTS = os.environ.get("QZ_REPLAY_ROUTED_EXPERTS", "1") == "1"
+REPLAY_GRAPHS = os.environ.get("QZ_REPLAY_GRAPHS", "1") == "1"  # capture the replay in a hipGraph
 
 
 class _RoutedExpertsReplay:
@@ -258,6 +259,7 @@ class _RoutedExpertsReplay:
     def __init__(self, module: nn.Module):
         self.m = module
         self.plans: Dict[Tuple[int, Tuple[int, ...]], Tuple[torch.Tensor, list]] = {}
+        self.graphs: Dict[Tuple[int, Tuple[int, ...]], Optional[tuple]] = {}
         self.changed: Optional[torch.Tensor] = None
         self.ok = True
 
@@ -314,12 +316,44 @@ class _RoutedExpertsReplay:
                          float((got.float() - want.float()).abs().max()),
                          "agrees with itself" if _bits_equal(again, want) else "DISAGREES with itself")
                 self.ok = False
+            elif REPLAY_GRAPHS and hidden_states.is_cuda:
+                self.graphs[key] = self._capture(hidden_states, top_k_weights, plan, got)
             return want
         idx0, plan = self.plans[key]
         diff = (top_k_index != idx0).any() if top_k_index.shape == idx0.shape else torch.ones((), dtype=torch.bool,
                                                                                                device=idx0.device)
         self.changed = diff if self.changed is None else (self.changed | diff)
-        return self._replay(hidden_states, top_k_weights, plan)
+        cap = self.graphs.get(key)
+        if cap is None:
+            return self._replay(hidden_states, top_k_weights, plan)
+        graph, static_w, out = cap
+        static_w.copy_(top_k_weights)
+        graph.replay()
+        return out
+
+    def _capture(self, hidden_states, top_k_weights, plan, check):
+        """The replay as one hipGraph (its ~9 launches per routed expert replayed by one graph
+        launch per grid point); the routing weights enter through a static copy, the output is
+        the graph's own buffer (consumed by the grid's loss before the next replay).  None if
+        capture fails or the captured replay is not bit-identical to the eager replay."""
+        try:
+            static_w = top_k_weights.clone()
+            side = torch.cuda.Stream(hidden_states.device)
+            side.wait_stream(torch.cuda.current_stream(hidden_states.device))
+            with torch.cuda.stream(side):
+                self._replay(hidden_states, static_w, plan)  # warm-up outside the capture
+            torch.cuda.current_stream(hidden_states.device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                out = self._replay(hidden_states, static_w, plan)
+            graph.replay()
+            if not _bits_equal(out, check):
+                log.info("AWQ: captured experts replay differs from the eager replay; not using the graph")
+                return None
+            return graph, static_w, out
+        except RuntimeError as e:  # capture unsupported for some op: keep the eager replay
+            log.info("AWQ: experts replay not captured (%s)", e)
+            return None
 
     def close(self) -> None:
         if self.changed is not None and bool(self.changed):

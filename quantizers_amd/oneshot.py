@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import os
 import threading
 import time
 from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
@@ -270,6 +271,9 @@ def _eager_experts(model: nn.Module):
     instead, which would move every MoE-parent loss and propagated activation off the
     reference's arithmetic.  In the eager form an AWQ grid with a MoE-block parent also replays
     its fixed routing without host syncs (awq._RoutedExpertsReplay)."""
+    if os.environ.get("QZ_EAGER_EXPERTS", "1") != "1":  # A/B knob: keep the model's own setting
+        yield
+        return
     cfgs = {}
     for mod in model.modules():
         c = getattr(mod, "config", None)
