@@ -36,7 +36,6 @@ per mapping).
 """
 from __future__ import annotations
 
-import contextlib
 import logging
 import os
 import re
@@ -239,160 +238,6 @@ class _ExpertInputs:
 
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
-REPLAY_ROUTED_EXPERTS = os.environ.get("QZ_REPLAY_ROUTED_EXPERTS", "1") == "1"
-REPLAY_GRAPHS = os.environ.get("QZ_REPLAY_GRAPHS", "1") == "1"  # capture the replay in a hipGraph
-
-
-class _RoutedExpertsReplay:
-    """The fused experts forward of transformers' MoE blocks (Qwen3-MoE, MiniMax-M2: one_hot of
-    the top-k choice, then per routed expert ``torch.where`` -> gather -> gate_up GEMM -> act * up
-    -> down GEMM -> routing weight -> ``index_add_``) synchronises with the host twice per expert
-    (``expert_idx == num_experts`` and the ``where``), so the 21 forwards of an AWQ grid whose
-    parent is the MoE block run host-bound (69 % GPU busy).  Inside such a grid the
-    block's input and router are unchanged, so the routing is too: the first call per input
-    records each routed expert's (positions, tokens) -- the same host work HF does -- and every
-    later call replays the SAME op sequence with those indices and no host sync.  The first
-    replay is checked bit for bit against the module's own forward (a mismatch keeps the
-    module's forward for this grid); later calls compare their routing with the recorded one on
-    the device and ``close`` raises if it ever changed."""
-
-    def __init__(self, module: nn.Module):
-        self.m = module
-        self.plans: Dict[Tuple[int, Tuple[int, ...]], Tuple[torch.Tensor, list]] = {}
-        self.graphs: Dict[Tuple[int, Tuple[int, ...]], Optional[tuple]] = {}
-        self.changed: Optional[torch.Tensor] = None
-        self.ok = True
-
-    @staticmethod
-    def applies(module: nn.Module) -> bool:
-        import inspect
-        if not (type(module).__name__.endswith("Experts") and hasattr(module, "gate_up_proj")
-                and hasattr(module, "down_proj") and hasattr(module, "act_fn") and hasattr(module, "num_experts")):
-            return False
-        try:
-            params = list(inspect.signature(type(module).forward).parameters)
-        except (TypeError, ValueError):
-            return False
-        return params[1:] == ["hidden_states", "top_k_index", "top_k_weights"]
-
-    def _plan(self, top_k_index: torch.Tensor) -> list:
-        with torch.no_grad():
-            mask = nn.functional.one_hot(top_k_index, num_classes=self.m.num_experts).permute(2, 1, 0)
-            hit = torch.greater(mask.sum(dim=(-1, -2)), 0).nonzero()
-            plan = []
-            for e in hit[:, 0].tolist():
-                if e == self.m.num_experts:
-                    continue
-                pos, tok = torch.where(mask[e])
-                plan.append((e, pos, tok))
-        return plan
-
-    def _replay(self, hidden_states, top_k_weights, plan):
-        m = self.m
-        final = torch.zeros_like(hidden_states)
-        for e, pos, tok in plan:
-            cur = hidden_states[tok]
-            gate, up = nn.functional.linear(cur, m.gate_up_proj[e]).chunk(2, dim=-1)
-            cur = m.act_fn(gate) * up
-            cur = nn.functional.linear(cur, m.down_proj[e])
-            cur = cur * top_k_weights[tok, pos, None]
-            final.index_add_(0, tok, cur.to(final.dtype))
-        return final
-
-    def forward(self, hidden_states, top_k_index, top_k_weights):
-        if not self.ok:
-            return type(self.m).forward(self.m, hidden_states, top_k_index, top_k_weights)
-        key = (hidden_states.data_ptr(), tuple(hidden_states.shape))
-        if key not in self.plans:
-            plan = self._plan(top_k_index)
-            self.plans[key] = (top_k_index.clone(), plan)
-            want = type(self.m).forward(self.m, hidden_states, top_k_index, top_k_weights)
-            got = self._replay(hidden_states, top_k_weights, plan)
-            if not _bits_equal(got, want):
-                again = type(self.m).forward(self.m, hidden_states, top_k_index, top_k_weights)
-                log.info("AWQ: routed-experts replay differs from %s.forward in %d of %d elements (max |d| %.3g; "
-                         "the module's forward run twice %s); using the module's own",
-                         type(self.m).__name__, int((got != want).sum()), want.numel(),
-                         float((got.float() - want.float()).abs().max()),
-                         "agrees with itself" if _bits_equal(again, want) else "DISAGREES with itself")
-                self.ok = False
-            elif REPLAY_GRAPHS and hidden_states.is_cuda:
-                self.graphs[key] = self._capture(hidden_states, top_k_weights, plan, got)
-            return want
-        idx0, plan = self.plans[key]
-        diff = (top_k_index != idx0).any() if top_k_index.shape == idx0.shape else torch.ones((), dtype=torch.bool,
-                                                                                               device=idx0.device)
-        self.changed = diff if self.changed is None else (self.changed | diff)
-        cap = self.graphs.get(key)
-        if cap is None:
-            return self._replay(hidden_states, top_k_weights, plan)
-        graph, static_w, out = cap
-        static_w.copy_(top_k_weights)
-        graph.replay()
-        return out
-
-    def _capture(self, hidden_states, top_k_weights, plan, check):
-        """The replay as one hipGraph (its ~9 launches per routed expert replayed by one graph
-        launch per grid point); the routing weights enter through a static copy, the output is
-        the graph's own buffer (consumed by the grid's loss before the next replay).  None if
-        capture fails or the captured replay is not bit-identical to the eager replay."""
-        try:
-            static_w = top_k_weights.clone()
-            side = torch.cuda.Stream(hidden_states.device)
-            side.wait_stream(torch.cuda.current_stream(hidden_states.device))
-            with torch.cuda.stream(side):
-                self._replay(hidden_states, static_w, plan)  # warm-up outside the capture
-            torch.cuda.current_stream(hidden_states.device).wait_stream(side)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                out = self._replay(hidden_states, static_w, plan)
-            graph.replay()
-            if not _bits_equal(out, check):
-                log.info("AWQ: captured experts replay differs from the eager replay; not using the graph")
-                return None
-            return graph, static_w, out
-        except RuntimeError as e:  # capture unsupported for some op: keep the eager replay
-            log.info("AWQ: experts replay not captured (%s)", e)
-            return None
-
-    def close(self) -> None:
-        if self.changed is not None and bool(self.changed):
-            raise RuntimeError("AWQ: the MoE routing changed inside a grid search (replay invalid)")
-
-
-def _bits_equal(a: torch.Tensor, b: torch.Tensor) -> bool:
-    if a.dtype != b.dtype or a.shape != b.shape:
-        return False
-    if a.dtype in (torch.bfloat16, torch.float16):
-        return torch.equal(a.view(torch.int16), b.view(torch.int16))
-    return torch.equal(a, b)
-
-
-class _ReplayExperts:
-    """Context: every transformers fused-experts module under ``parent`` forwards through a
-    ``_RoutedExpertsReplay`` (REPLAY_ROUTED_EXPERTS; the module's own forward otherwise)."""
-
-    def __init__(self, parent: nn.Module):
-        self.mods = [m for m in parent.modules() if REPLAY_ROUTED_EXPERTS and _RoutedExpertsReplay.applies(m)]
-        self.replays: List[_RoutedExpertsReplay] = []
-
-    def __enter__(self):
-        for m in self.mods:
-            rp = _RoutedExpertsReplay(m)
-            m.forward = rp.forward  # instance attribute: Module.__call__ dispatches to it
-            self.replays.append(rp)
-        return self
-
-    def __exit__(self, *exc):
-        for m in self.mods:
-            if "forward" in m.__dict__:
-                del m.forward
-        if exc[0] is None:
-            for rp in self.replays:
-                rp.close()
-        return False
-
-
 def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
     if ref.param_name == "down_proj" or ref.param_name == "w2":
         return ei.hidden(i, ref.index[0])
@@ -752,9 +597,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                         gate, up = nn.functional.linear(t, mod.gate_up_proj[e]).chunk(2, dim=-1)
                         outs.append(nn.functional.linear(mod.act_fn(gate) * up, mod.down_proj[e]))
                     return outs
-        # a MoE-block parent: its experts forward replays the (fixed) routing without host syncs
-        with _ReplayExperts(r.parent) if r.parent_kind == "module" else contextlib.nullcontext():
-            return _grid(r, groups, run, x_mean, w_mean, grid_shard)
+        return _grid(r, groups, run, x_mean, w_mean, grid_shard)
 
     def _grid(r, groups, run, x_mean, w_mean, grid_shard):
         """Steps 3-4 of ``search``: the 20-point grid and its argmin."""

@@ -1,0 +1,129 @@
+"""transformers' fused MoE experts in the reference's arithmetic, at grouped-GEMM speed.
+
+The reference pins transformers 4.57, whose MoE blocks loop over per-expert Linear modules: per
+routed expert, gather its tokens, gate / up GEMM, ``act(gate) * up``, down GEMM, times the
+routing weight, ``index_add_`` into a bf16 accumulator -- so every token sums its top-k
+contributions in ascending expert order with a bf16 rounding after each add.  transformers 5
+keeps that loop as the experts' ``eager`` form (with two host syncs per expert) and defaults to
+a ``grouped_mm`` form that sums the top-k contributions in f32 -- different bits in about half
+of the outputs (``profiles/r02at_fast_eager.log``).
+
+``FastEagerExperts`` computes the eager result with two grouped GEMMs (tokens sorted by expert:
+hipBLASLt gives every row the same bits as the per-expert GEMM), the routing weight, and k
+sequential bf16 adds in ascending expert order -- no host sync, ~10 launches instead of ~9 per
+expert.  The first call per input shape is checked bit for bit against the module's own eager
+forward; a mismatch makes that module use the eager forward for the rest of the pass.
+Decision D15: the AWQ pass runs MoE experts in this eager arithmetic."""
+from __future__ import annotations
+
+import contextlib
+import inspect
+import logging
+import os
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+from torch import nn
+
+log = logging.getLogger(__name__)
+
+FAST_EAGER = os.environ.get("QZ_FAST_EAGER_EXPERTS", "1") == "1"  # A/B knob: 0 = the eager loop itself
+
+
+def eager_forward(module: nn.Module) -> Optional[Callable]:
+    """The experts class's eager forward (the function transformers' ``use_experts_implementation``
+    wraps), or None for a module that is not a transformers fused-experts module."""
+    if not (type(module).__name__.endswith("Experts") and hasattr(module, "gate_up_proj")
+            and hasattr(module, "down_proj") and hasattr(module, "act_fn") and hasattr(module, "num_experts")):
+        return None
+    if getattr(module, "has_bias", False) or getattr(module, "is_transposed", False) \
+            or not getattr(module, "is_concatenated", True) or not getattr(module, "has_gate", True):
+        return None
+    fwd = type(module).forward
+    fwd = getattr(fwd, "__wrapped__", fwd)
+    try:
+        params = list(inspect.signature(fwd).parameters)
+    except (TypeError, ValueError):
+        return None
+    return fwd if params[1:] == ["hidden_states", "top_k_index", "top_k_weights"] else None
+
+
+def _bits_equal(a: torch.Tensor, b: torch.Tensor) -> bool:
+    if a.dtype != b.dtype or a.shape != b.shape:
+        return False
+    if a.dtype in (torch.bfloat16, torch.float16):
+        return torch.equal(a.view(torch.int16), b.view(torch.int16))
+    return torch.equal(a, b)
+
+
+def fast_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Tensor,
+               top_k_weights: torch.Tensor) -> torch.Tensor:
+    """The eager experts result without host syncs (see the module docstring)."""
+    t, k = top_k_index.shape
+    flat = top_k_index.reshape(-1)
+    _, perm = torch.sort(flat, stable=True)  # (token, slot) pairs grouped by expert
+    counts = torch.zeros(m.num_experts, dtype=torch.int64, device=flat.device).scatter_add_(
+        0, flat, torch.ones_like(flat))
+    offs = counts.cumsum(0).to(torch.int32)
+    xg = hidden_states[perm // k]
+    gate, up = nn.functional.grouped_mm(xg, m.gate_up_proj.transpose(-2, -1), offs=offs).chunk(2, dim=-1)
+    h = m.act_fn(gate) * up
+    d = nn.functional.grouped_mm(h, m.down_proj.transpose(-2, -1), offs=offs)
+    d = d * top_k_weights.reshape(-1)[perm][:, None]
+    contrib = torch.empty_like(d)
+    contrib[perm] = d
+    contrib = contrib.view(t, k, -1)
+    order = torch.argsort(top_k_index, dim=-1)  # each token's experts in ascending id: the eager add order
+    contrib = torch.gather(contrib, 1, order[:, :, None].expand(-1, -1, contrib.shape[-1]))
+    final = torch.zeros_like(hidden_states)
+    for j in range(k):
+        final = final + contrib[:, j].to(final.dtype)
+    return final
+
+
+class FastEagerExperts:
+    """Instance-level forward for one experts module (see the module docstring)."""
+
+    checked: Dict[Tuple, bool] = {}  # (class, shape, dtype) -> fast path verified; shared per pass
+
+    def __init__(self, module: nn.Module, eager: Callable):
+        self.m = module
+        self.eager = eager
+
+    def forward(self, hidden_states, top_k_index, top_k_weights):
+        if not FAST_EAGER or not hasattr(nn.functional, "grouped_mm"):
+            return self.eager(self.m, hidden_states, top_k_index, top_k_weights)
+        key = (type(self.m).__name__, tuple(hidden_states.shape), tuple(top_k_index.shape), hidden_states.dtype,
+               tuple(self.m.gate_up_proj.shape))
+        ok = FastEagerExperts.checked.get(key)
+        if ok is None:
+            want = self.eager(self.m, hidden_states, top_k_index, top_k_weights)
+            got = fast_eager(self.m, hidden_states, top_k_index, top_k_weights)
+            ok = _bits_equal(got, want)
+            FastEagerExperts.checked[key] = ok
+            if not ok:
+                log.info("MoE: grouped eager form differs from %s's eager forward at %s; using the eager loop",
+                         type(self.m).__name__, key[1])
+            return want
+        if not ok:
+            return self.eager(self.m, hidden_states, top_k_index, top_k_weights)
+        return fast_eager(self.m, hidden_states, top_k_index, top_k_weights)
+
+
+@contextlib.contextmanager
+def eager_experts(model: nn.Module):
+    """Every transformers fused-experts module of ``model`` forwards in the eager arithmetic
+    (``FastEagerExperts``) inside the context; the modules' own forwards are restored after."""
+    patched = []
+    FastEagerExperts.checked = {}
+    try:
+        for mod in model.modules():
+            fwd = eager_forward(mod)
+            if fwd is not None:
+                mod.forward = FastEagerExperts(mod, fwd).forward  # instance attribute: Module.__call__ uses it
+                patched.append(mod)
+        yield len(patched)
+    finally:
+        for mod in patched:
+            if "forward" in mod.__dict__:
+                del mod.forward

@@ -13,9 +13,7 @@ scheme of each targeted module (same names as the reference's per-expert Linear 
 """
 from __future__ import annotations
 
-import contextlib
 import logging
-import os
 import threading
 import time
 from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
@@ -24,6 +22,7 @@ import torch
 from torch import nn
 
 from . import awq as awq_mod
+from .moe_eager import eager_experts
 from .model import checkpoint_name, decoder_layers, iter_linears, model_type
 from .quantization import QuantizationScheme
 from .recipe import AWQModifier, QuantizationModifier, match_any, match_precedence, parse_recipe
@@ -186,7 +185,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                 # embeddings / rotary / final norm run on the device; layers are onloaded one
                 # by one (the reference's sequential-pipeline placement)
                 _to_device_except(model, decoder_layers(model), device)
-        with _eager_experts(model):
+        # MoE experts in the reference's (transformers 4.57) eager arithmetic, at grouped speed (D15)
+        with eager_experts(model):
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
                                 stateful_observers)
@@ -260,33 +260,6 @@ def _offload(module: nn.Module, host: Dict) -> None:
                     t.data = h
                 else:
                     store[name] = h
-
-
-@contextlib.contextmanager
-def _eager_experts(model: nn.Module):
-    """Run transformers' fused MoE experts in their eager form (per routed expert: GEMMs, routing
-    weight, bf16 ``index_add_`` in expert order) for the duration of the AWQ pass (decision D15).
-    The reference pins transformers 4.57, whose MoE blocks loop over per-expert Linear modules
-    exactly so; transformers 5's default ``grouped_mm`` form sums the top-k contributions in f32
-    instead, which would move every MoE-parent loss and propagated activation off the
-    reference's arithmetic.  In the eager form an AWQ grid with a MoE-block parent also replays
-    its fixed routing without host syncs (awq._RoutedExpertsReplay)."""
-    if os.environ.get("QZ_EAGER_EXPERTS", "1") != "1":  # A/B knob: keep the model's own setting
-        yield
-        return
-    cfgs = {}
-    for mod in model.modules():
-        c = getattr(mod, "config", None)
-        if c is not None and hasattr(c, "_experts_implementation") and c._experts_implementation not in (None, "eager"):
-            cfgs[id(c)] = c
-    old = {k: c._experts_implementation for k, c in cfgs.items()}
-    try:
-        for c in cfgs.values():
-            c._experts_implementation = "eager"
-        yield
-    finally:
-        for k, c in cfgs.items():
-            c._experts_implementation = old[k]
 
 
 def _fits_on_device(model: nn.Module, device) -> bool:
