@@ -238,6 +238,7 @@ class _ExpertInputs:
 
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
+EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches: experts outer, grid inner
 def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
     if ref.param_name == "down_proj" or ref.param_name == "w2":
         return ei.hidden(i, ref.index[0])
@@ -695,11 +696,25 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         wq = torch.empty_like(w0)
         scales = torch.empty(n_grid, len(refs), cols, dtype=torch.float32, device=w2.device)
         losses = torch.zeros(n_grid, len(refs), dtype=torch.float64, device=w2.device)
-        for g in range(n_grid):
-            ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
-            ops.fake_quantize_batched(w0, a, scales[g], out=wq)
+        if EXPERT_MAJOR:
+            # every grid point's fake-quantized weights first, then expert by expert over the grid:
+            # an expert's inputs and reference output are re-read 20 times back to back (from the
+            # 256 MB Infinity Cache where they fit) instead of once per pass over all experts.
+            # Same GEMM and loss per (grid point, expert): bit-identical losses.
+            wq_all = torch.empty((n_grid,) + tuple(w0.shape), dtype=w0.dtype, device=w0.device)
+            for g in range(n_grid):
+                ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
+                ops.fake_quantize_batched(w0, a, scales[g], out=wq_all[g])
             for k, (h, ro) in enumerate(zip(hs, ref_out)):
-                ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq[k]), losses[g, k:k + 1])
+                for g in range(n_grid):
+                    ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq_all[g, k]), losses[g, k:k + 1])
+            del wq_all
+        else:
+            for g in range(n_grid):
+                ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
+                ops.fake_quantize_batched(w0, a, scales[g], out=wq)
+                for k, (h, ro) in enumerate(zip(hs, ref_out)):
+                    ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq[k]), losses[g, k:k + 1])
         hist = (losses / max(n_el, 1)).cpu()
         out = []
         for k in range(len(refs)):
