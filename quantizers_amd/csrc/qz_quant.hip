@@ -713,12 +713,32 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
   return make_uint4(pk_bf16(q[0]), pk_bf16(q[1]), pk_bf16(q[2]), pk_bf16(q[3]));
 }
 
+// QZ_FQ_TILES > 1: a wave walks that many consecutive row tiles, loading tile t+1 before it
+// computes tile t (A/B knob; 1 = one tile per wave)
+#ifndef QZ_FQ_TILES
+#define QZ_FQ_TILES 1
+#endif
+constexpr int FQ_TILES = QZ_FQ_TILES;
+
+template <bool NT, int U>
+__device__ __forceinline__ void fq_load_tile(uint4 (&v)[U], const uint4* src, int64_t r0, int64_t rows, int64_t upr,
+                                             int64_t cuc) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    int64_t r = r0 + u;
+    r = r < rows ? r : rows - 1;
+    const uint4* ptr = src + r * upr + cuc;
+    if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr)));
+    else v[u] = *ptr;
+  }
+}
+
 template <int LOGL, int KIND, bool SYM, bool NT>
 __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   constexpr int U = FQ_ROWS;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + (threadIdx.x >> 6);
-  if (rblk * U >= rows) return;
+  const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + (threadIdx.x >> 6);  // a block of FQ_TILES tiles
+  if (rblk * U * FQ_TILES >= rows) return;
   const int64_t b = blockIdx.z;
   const int64_t upr = A.units_per_row;
   const int64_t cu = (int64_t)blockIdx.x * WAVE + lane;  // this lane's column unit
@@ -726,14 +746,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   const int64_t cuc = col_ok ? cu : upr - 1;
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
   uint4 v[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    int64_t r = rblk * U + u;
-    r = r < rows ? r : rows - 1;
-    const uint4* ptr = src + r * upr + cuc;
-    if constexpr (NT) v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr)));
-    else v[u] = *ptr;
-  }
+  fq_load_tile<NT, U>(v, src, rblk * U * FQ_TILES, rows, upr, cuc);
   // this lane's 8 column scales, their reciprocals, and whether rcp is accurate for all 8
   const float* csp = A.col_scales + b * A.cs_ld_batch + cuc * 8;
   const float4 c_lo = *reinterpret_cast<const float4*>(csp);
@@ -748,13 +761,25 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
              (fabsf(cs[k].y) <= 0x1.0p+100f);
   }
   const QP p = A.p;
-  uint4* dst = reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + rblk * U * upr + cuc;
-  const int nrow = (int)min<int64_t>(U, rows - rblk * U);  // rows of this tile inside the slice
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
-    if (col_ok && u < nrow) st_out<false>(dst, o);
-    dst += upr;
+  for (int t = 0; t < FQ_TILES; ++t) {
+    const int64_t r0 = (rblk * FQ_TILES + t) * U;
+    if (r0 >= rows) break;  // wave-uniform
+    uint4 nv[U];
+    const bool more = t + 1 < FQ_TILES && r0 + U < rows;
+    if (more) fq_load_tile<NT, U>(nv, src, r0 + U, rows, upr, cuc);  // in flight while tile t computes
+    uint4* dst = reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + r0 * upr + cuc;
+    const int nrow = (int)min<int64_t>(U, rows - r0);  // rows of this tile inside the slice
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
+      if (col_ok && u < nrow) st_out<false>(dst, o);
+      dst += upr;
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = nv[u];
+    }
   }
 }
 
@@ -1436,7 +1461,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
 #ifndef QZ_FQ_COLS
 #define QZ_FQ_COLS 1  // column-tiled AWQ fake-quant kernel (0: unit-wise k_group_fast, A/B knob)
 #endif
-    const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS), FBLOCK / WAVE);
+    const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS * FQ_TILES), FBLOCK / WAVE);
     FqcFn fqc = (QZ_FQ_COLS && fq && col_scales) ? pick_fqc(logl, pl.kind, pl.p.sym != 0, nt) : nullptr;
     if (fqc && fq_yblocks <= 65535) {
       hipLaunchKernelGGL(fqc, dim3((unsigned)cdiv(F.units_per_row, WAVE), (unsigned)fq_yblocks, (unsigned)batch),
