@@ -511,6 +511,27 @@ def test_moe_fast_eager_experts(cuda, monkeypatch, arch):
         _eq(p1[n], p0[n], n)
 
 
+@pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS"])
+def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
+    """The expert-search speed knobs (experts-outer order; one GEMM for the per-expert inputs)
+    change nothing: loss histories and smoothed parameters equal with the knob on and off."""
+    import quantizers_amd.awq as awq_mod
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(awq_mod, knob, on)
+        m = _minimax(layers=1, experts=4).to(cuda)
+        oneshot(m, os.path.join(ROOT, "configs/recipes/minimax_awq_mixedprec.yaml"), dataset=_calib(vocab=256),
+                max_seq_length=64)
+        out[on] = (m.awq_report, {n: p.detach().clone() for n, p in m.named_parameters()})
+    (r1, p1), (r0, p0) = out[True], out[False]
+    assert r1.keys() == r0.keys() and sum(len(v) for v in r1.values()) >= 4
+    for layer in r1:
+        for smooth, r in r1[layer].items():
+            assert r.get("history") == r0[layer][smooth].get("history"), (layer, smooth)
+    for n in p1:
+        _eq(p1[n], p0[n], n)
+
+
 def test_minimax_awq_mixedprec_end_to_end(cuda, tmp_path):
     """recipe_Minimax-M2.1-AWQ-MixedPrec semantics on a tiny random MiniMax-M2: FP8 g32 attention,
     int4 g32 experts, AWQ over attention, all experts' w1/w3 and each expert's w3 -> w2."""
