@@ -149,6 +149,43 @@ def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
     return out
 
 
+_SAMPLES: List[int] = [0]  # > 0 while a batched layer call stands for that many calibration samples
+
+
+def _split_samples(x: torch.Tensor) -> List[torch.Tensor]:
+    """Inside a batched calibration call (``_SAMPLES[0]`` = n samples stacked sample-major): the
+    per-sample pieces of a hooked input -- [n, S, ...] split along dim 0, a flattened [n * S, ...]
+    into n equal row blocks -- i.e. exactly what the per-sample calls handed the hook."""
+    n = _SAMPLES[0]
+    if n <= 1:
+        return [x]
+    if x.dim() >= 3 and x.shape[0] == n:
+        return [x[i:i + 1] for i in range(n)]
+    if x.shape[0] % n == 0:
+        return list(x.chunk(n, dim=0))
+    raise RuntimeError(f"AWQ: cannot split a hooked input of shape {tuple(x.shape)} into {n} samples")
+
+
+def stack_layer_calls(layer_inputs: List[Tuple[tuple, dict]]) -> Optional[Tuple[tuple, dict]]:
+    """The per-sample decoder-layer calls as ONE call with the hidden states stacked along the
+    batch dimension, when every other argument is the same for all samples and broadcasts over
+    the batch (same sequence length, same positions / rotary tables / mask); else None."""
+    if len(layer_inputs) < 2:
+        return None
+    a0, k0 = layer_inputs[0]
+    if not a0 or not torch.is_tensor(a0[0]) or a0[0].dim() != 3 or a0[0].shape[0] != 1:
+        return None
+    for a, k in layer_inputs[1:]:
+        if len(a) != len(a0) or not torch.is_tensor(a[0]) or a[0].shape != a0[0].shape \
+                or not _same(tuple(a[1:]), tuple(a0[1:])) or not _same(k, k0):
+            return None
+    for v in list(a0[1:]) + list(k0.values()):
+        for t in (v if isinstance(v, (tuple, list)) else (v,)):
+            if torch.is_tensor(t) and t.dim() >= 3 and t.shape[0] != 1:
+                return None
+    return (torch.cat([a[0] for a, _ in layer_inputs], dim=0),) + tuple(a0[1:]), dict(k0)
+
+
 class _ParentCache:
     """Forward pre-hook on a parent module: cache its (args, kwargs) per calibration batch."""
 
@@ -172,7 +209,8 @@ class _AbsMean:
         self.h = module.register_forward_pre_hook(self._hook) if module is not None else None
 
     def _hook(self, mod, args):
-        self.add(args[0])
+        for x in _split_samples(args[0]):  # one add per calibration sample, as per-sample calls did
+            self.add(x)
 
     def add(self, x: torch.Tensor):
         if self.sum is None:
@@ -202,8 +240,10 @@ class _ExpertInputs:
         self.h = module.register_forward_pre_hook(self._hook)
 
     def _hook(self, mod, args):
-        self.x.append(args[0].detach())
-        self.topk.append(args[1].detach() if len(args) > 1 and torch.is_tensor(args[1]) else None)
+        xs = _split_samples(args[0].detach())
+        tk = _split_samples(args[1].detach()) if len(args) > 1 and torch.is_tensor(args[1]) else [None] * len(xs)
+        self.x.extend(xs)
+        self.topk.extend(tk)
 
     def remove(self):
         self.h.remove()
@@ -515,13 +555,16 @@ def _expert_chunk(n_tokens: int, inter: int, hidden: int, budget: int = 4 << 30)
 def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dict]], mappings: List[AWQMapping],
               quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20,
               mtype: str = "", calibrate_all_experts: bool = True,
-              stateful_observers: bool = False) -> Dict[str, Any]:
+              stateful_observers: bool = False, batched_calls: bool = False) -> Dict[str, Any]:
     """Run AWQ on one decoder layer in place.  ``layer_inputs`` are the cached (args, kwargs)
     of the layer for every calibration batch.  Returns per-mapping diagnostics.
 
     ``stateful_observers``: balance layers whose scheme names the ``minmax`` / ``static_minmax``
     observer keep that observer's memory across the 20 grid points of their search (D7's
-    stateful reading); default: every observation is memoryless (D7)."""
+    stateful reading); default: every observation is memoryless (D7).
+    ``batched_calls``: run the calibration pass as one call over the stacked samples
+    (``stack_layer_calls``; the hooks see the same per-sample inputs) -- the caller has checked
+    that the batched layer forward is bit-identical to the per-sample one."""
     resolved = resolve_mappings(layer, prefix, mappings, quantized, mtype)
     if not resolved:
         return {}
@@ -544,9 +587,17 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         elif id(r.balance[0].module) not in experts:
             experts[id(r.balance[0].module)] = _ExpertInputs(r.balance[0].module, calibrate_all_experts)
             hooks.append(experts[id(r.balance[0].module)])
+    stacked = stack_layer_calls(layer_inputs) if batched_calls else None
     try:
-        for args, kwargs in layer_inputs:
-            layer(*args, **kwargs)
+        if stacked is not None:  # one batched call; the hooks split it back into the samples
+            _SAMPLES[0] = len(layer_inputs)
+            try:
+                layer(*stacked[0], **stacked[1])
+            finally:
+                _SAMPLES[0] = 0
+        else:
+            for args, kwargs in layer_inputs:
+                layer(*args, **kwargs)
     finally:
         for h in hooks:
             h.remove()

@@ -14,6 +14,7 @@ scheme of each targeted module (same names as the reference's per-expert Linear 
 from __future__ import annotations
 
 import logging
+import os
 import threading
 import time
 from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
@@ -120,6 +121,7 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
     inputs = _capture_layer0_inputs(model, layers, batches)
     mtype = model_type(model)
     stager = None
+    batched: Optional[bool] = None  # per-sample layer calls run as one batched call (checked on layer 0)
     for i, layer in enumerate(layers):
         home = next(layer.parameters()).device
         host = None
@@ -129,14 +131,21 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
                 stager = H2DStager(device)
             host = _onload(layer, stager)
         t0 = time.time()
+        if batched is None:
+            batched = BATCH_LAYER_CALLS and _batched_forward_ok(layer, inputs)
         rep = awq_mod.awq_layer(layer, checkpoint_name(f"{lname}.{i}", mtype), inputs, mappings, weights,
                                 awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts,
-                                stateful_observers=stateful_observers)
+                                stateful_observers=stateful_observers, batched_calls=batched)
         report[f"{lname}.{i}"] = rep
-        nxt = []
-        for args, kwargs in inputs:
-            out = _layer_out(layer(*args, **kwargs))
-            nxt.append(((out,) + tuple(args[1:]), kwargs))
+        stacked = awq_mod.stack_layer_calls(inputs) if batched else None
+        if stacked is not None:  # propagate all samples in one call, split back per sample
+            out = _layer_out(layer(*stacked[0], **stacked[1]))
+            nxt = [((out[j:j + 1],) + tuple(args[1:]), kwargs) for j, (args, kwargs) in enumerate(inputs)]
+        else:
+            nxt = []
+            for args, kwargs in inputs:
+                out = _layer_out(layer(*args, **kwargs))
+                nxt.append(((out,) + tuple(args[1:]), kwargs))
         inputs = nxt
         if host is not None:
             _offload(layer, host)
@@ -198,6 +207,26 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         from .compressor import save_compressed
         save_compressed(model, output_dir)
     return model
+
+
+BATCH_LAYER_CALLS = os.environ.get("QZ_BATCH_LAYER_CALLS", "1") == "1"
+
+
+@torch.no_grad()
+def _batched_forward_ok(layer: nn.Module, inputs) -> bool:
+    """Is the decoder layer's forward over the stacked samples bit-identical to its per-sample
+    forwards?  (Row- and sequence-independent kernels make it so on this stack; checked once, on
+    the first layer, before anything is batched.)"""
+    stacked = awq_mod.stack_layer_calls(inputs)
+    if stacked is None:
+        return False
+    per = [_layer_out(layer(*a, **k)) for a, k in inputs]
+    out = _layer_out(layer(*stacked[0], **stacked[1]))
+    ok = all(torch.equal(out[j:j + 1].view(torch.int16), p.view(torch.int16)) if p.dtype == torch.bfloat16
+             else torch.equal(out[j:j + 1], p) for j, p in enumerate(per))
+    log.info("AWQ: per-sample layer calls %s as one batched call of %d", "run" if ok else "NOT run (bits differ)",
+             len(inputs))
+    return ok
 
 
 @torch.no_grad()

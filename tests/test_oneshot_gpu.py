@@ -532,6 +532,33 @@ def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
         _eq(p1[n], p0[n], n)
 
 
+@pytest.mark.parametrize("arch", ["qwen3", "qwen3_moe", "minimax"])
+def test_batched_layer_calls_bit_identical(cuda, monkeypatch, arch):
+    """The calibration and propagation passes run the stacked samples as one layer call (hooks
+    split it back per sample): loss histories, smoothed parameters and the checkpoint tensors
+    equal the per-sample passes."""
+    import quantizers_amd.oneshot as os_mod
+    build = {"qwen3": _qwen3, "qwen3_moe": _qwen3_moe, "minimax": _minimax}[arch]
+    recipe = os.path.join(ROOT, "configs", "recipes",
+                          "minimax_awq_mixedprec.yaml" if arch == "minimax" else "awq_w4a16_g32.yaml")
+    out = {}
+    for on in (True, False):
+        monkeypatch.setattr(os_mod, "BATCH_LAYER_CALLS", on)
+        m = build().to(cuda)
+        oneshot(m, recipe, dataset=_calib(vocab=256), max_seq_length=64)
+        out[on] = (m.awq_report, {n: p.detach().clone() for n, p in m.named_parameters()}, compressed_state_dict(m))
+    (r1, p1, s1), (r0, p0, s0) = out[True], out[False]
+    assert r1.keys() == r0.keys()
+    for layer in r1:
+        for smooth, r in r1[layer].items():
+            assert r.get("history") == r0[layer][smooth].get("history"), (layer, smooth)
+    for n in p1:
+        _eq(p1[n], p0[n], n)
+    assert s1.keys() == s0.keys()
+    for k in s1:
+        _eq(s1[k], s0[k], k)
+
+
 def test_minimax_awq_mixedprec_end_to_end(cuda, tmp_path):
     """recipe_Minimax-M2.1-AWQ-MixedPrec semantics on a tiny random MiniMax-M2: FP8 g32 attention,
     int4 g32 experts, AWQ over attention, all experts' w1/w3 and each expert's w3 -> w2."""
