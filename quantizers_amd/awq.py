@@ -279,6 +279,46 @@ class _ExpertInputs:
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches: experts outer, grid inner
+OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "1") == "1"  # expert searches: loss kernels on a side stream
+
+
+def _overlapped_losses(hs, ref_out, wq_all, losses) -> None:
+    """Expert-major grid losses with each loss kernel (memory-bound) on a side stream, so it runs
+    beside the next GEMM (MFMA-bound) instead of after it.  The GEMM outputs alternate between two
+    buffers (a GEMM waits for the loss that last read its buffer); the GEMM is ``mm(h, W^T)``, the
+    same call ``F.linear`` makes, and every loss accumulates into its own slot: the same bits."""
+    dev = hs[0].device
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(main)
+    n_grid = wq_all.shape[0]
+    bufs = [torch.empty(ref_out[0].shape, dtype=ref_out[0].dtype, device=dev) for _ in range(2)]
+    done: List[Optional[torch.cuda.Event]] = [None, None]
+    step = 0
+    for k, (h, ro) in enumerate(zip(hs, ref_out)):
+        if ro.shape != bufs[0].shape:
+            bufs = [torch.empty(ro.shape, dtype=ro.dtype, device=dev) for _ in range(2)]
+            done = [None, None]
+            side.wait_stream(main)
+            main.wait_stream(side)
+        for g in range(n_grid):
+            i = step % 2
+            if done[i] is not None:
+                main.wait_event(done[i])
+            torch.mm(h.reshape(-1, h.shape[-1]), wq_all[g, k].t(), out=bufs[i].view(-1, bufs[i].shape[-1]))
+            ready = torch.cuda.Event()
+            ready.record(main)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                ops.awq_sq_err_accum(ro, bufs[i], losses[g, k:k + 1])
+                done[i] = torch.cuda.Event()
+                done[i].record(side)
+            step += 1
+    main.wait_stream(side)
+    for b in bufs:
+        b.record_stream(side)
+
+
 def _virtual_input(ei: _ExpertInputs, ref: LinearRef, i: int) -> torch.Tensor:
     if ref.param_name == "down_proj" or ref.param_name == "w2":
         return ei.hidden(i, ref.index[0])
@@ -756,9 +796,12 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             for g in range(n_grid):
                 ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
                 ops.fake_quantize_batched(w0, a, scales[g], out=wq_all[g])
-            for k, (h, ro) in enumerate(zip(hs, ref_out)):
-                for g in range(n_grid):
-                    ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq_all[g, k]), losses[g, k:k + 1])
+            if OVERLAP_LOSS and w0.is_cuda:
+                _overlapped_losses(hs, ref_out, wq_all, losses)
+            else:
+                for k, (h, ro) in enumerate(zip(hs, ref_out)):
+                    for g in range(n_grid):
+                        ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq_all[g, k]), losses[g, k:k + 1])
             del wq_all
         else:
             for g in range(n_grid):
