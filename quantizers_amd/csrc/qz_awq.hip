@@ -25,50 +25,91 @@ int launch_err() {
 }
 
 // ---------------------------------------------------------- a3: sum_t |x[t, c]|
-// stage 1: block = 4 waves over 512 channels (lane = 8 channels, one 16-B load) x a chunk of tc
-// tokens; wave w takes tokens w, w+4, ... (4 independent loads in flight per lane), the 4 wave
-// sums are added in a fixed order through LDS -> partial[chunk][c]
-__global__ __launch_bounds__(256) void k_absmean_partial_v8(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
-                                                            int64_t tc, float* part) {
-  __shared__ float red[4][512];
+// Both statistics reduce a tall [rows, C] bf16 matrix into per-column sums with the same stage-1
+// shape: a workgroup of SWP waves covers one 512-column window (lane = 8 columns, one 16-B load
+// per row) x a chunk of rows; wave w takes rows w, w + SWP, ... in order, SNB rows per batch, and
+// the next batch's loads are issued before the current batch is summed (software pipelined: a
+// wave always has SNB 16-B loads in flight while it computes).  Load addresses are clamped into
+// the matrix so no load is predicated (the compiler can then count vmcnt instead of draining);
+// rows past the chunk end are skipped by a wave-uniform branch.  The SWP wave sums are added in a
+// fixed order (((s0 + s1) + s2) + ...) through LDS -> part[chunk][c]; stage 2 (k_colsum_final)
+// adds the chunks in a fixed order: deterministic.
+#ifndef QZ_ABSMEAN_WPB
+#define QZ_ABSMEAN_WPB 8  // tuning knob: waves per absmean stage-1 workgroup
+#endif
+#ifndef QZ_WMEAN_WPB
+#define QZ_WMEAN_WPB 8  // tuning knob: waves per w_mean stage-1 workgroup
+#endif
+#ifndef QZ_ABSMEAN_NB
+#define QZ_ABSMEAN_NB 8  // tuning knob: activation rows per batch (loads in flight per lane)
+#endif
+#ifndef QZ_WMEAN_NB
+#define QZ_WMEAN_NB 4  // tuning knob: weight rows per batch (f64 sums: fewer, to keep VGPRs < 128)
+#endif
+constexpr int AWP = QZ_ABSMEAN_WPB, WWP = QZ_WMEAN_WPB;
+
+// walk rows r0 + wv, r0 + wv + SWP, ... < r1 of the 8 columns at col (clamped into [0, C - 8]);
+// f(v) is called once per row in row order
+template <int SWP, int SNB, typename F>
+__device__ __forceinline__ void stats_rows(const uint16_t* base, int64_t ld, int64_t r0, int64_t r1, int wv, F&& f) {
+  // row offsets in 32 x 32 -> 64-bit products (one v_mad_u64_u32; the host guarantees rows and
+  // ld < 2^31)
+  const uint32_t rlast = (uint32_t)(r1 - 1), uld = (uint32_t)ld;
+  auto ld16 = [&](int64_t r) {
+    return *reinterpret_cast<const uint4*>(base + (uint64_t)std::min((uint32_t)r, rlast) * uld);
+  };
+  int64_t r = r0 + wv;
+  if (r >= r1) return;
+  uint4 cur[SNB];
+#pragma unroll
+  for (int j = 0; j < SNB; ++j) cur[j] = ld16(r + (int64_t)j * SWP);
+  // in the loop the next batch starts inside the chunk, so every row of the current one is valid
+  for (; r + (int64_t)SNB * SWP < r1; r += (int64_t)SNB * SWP) {
+    uint4 nxt[SNB];
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) nxt[j] = ld16(r + (int64_t)(SNB + j) * SWP);
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) f(cur[j]);
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) cur[j] = nxt[j];
+  }
+#pragma unroll
+  for (int j = 0; j < SNB; ++j)
+    if (r + (int64_t)j * SWP < r1) f(cur[j]);
+}
+
+template <int SWP, typename T>
+__device__ __forceinline__ void stats_block_sum(T (*red)[512], const T* acc, int lane, int wv, int64_t C, T* dst) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
+  __syncthreads();
+  for (int j = threadIdx.x; j < 512; j += SWP * 64) {
+    const int64_t c = (int64_t)blockIdx.x * 512 + j;
+    if (c < C) {
+      T t = red[0][j];
+#pragma unroll
+      for (int w = 1; w < SWP; ++w) t += red[w][j];
+      dst[c] = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(AWP * 64) void k_absmean_partial_v8(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                                                 int64_t tc, float* part) {
+  __shared__ float red[AWP][512];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * 512 + lane * 8;
-  const bool in = c0 < C;
+  const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * 512 + lane * 8, C - 8);
   const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  auto add = [&](const uint4 v) {
+  stats_rows<AWP, QZ_ABSMEAN_NB>(x + c0, ld, t0, t1, wv, [&](const uint4 v) {
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       acc[2 * k] += fabsf(__uint_as_float(w[k] << 16));
       acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
     }
-  };
-  if (in) {
-    int64_t t = t0 + wv;
-    for (; t + 28 < t1; t += 32) {  // 8 token loads in flight per lane
-      uint4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const uint4*>(x + (t + 4 * j) * ld + c0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) add(v[j]);
-    }
-    for (; t + 12 < t1; t += 16) {
-      uint4 v[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const uint4*>(x + (t + 4 * j) * ld + c0);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) add(v[j]);
-    }
-    for (; t < t1; t += 4) add(*reinterpret_cast<const uint4*>(x + t * ld + c0));
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
-  __syncthreads();
-  for (int j = threadIdx.x; j < 512; j += 256) {
-    const int64_t c = (int64_t)blockIdx.x * 512 + j;
-    if (c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
-  }
+  });
+  stats_block_sum<AWP>(red, acc, lane, wv, C, part + (int64_t)blockIdx.y * C);
 }
 __global__ __launch_bounds__(256) void k_absmean_partial_v1(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
                                                             int64_t tc, float* part) {
@@ -166,7 +207,7 @@ int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
 #define QZ_ABSMEAN_MIN_TC 128  // tuning knob: minimum tokens per stage-1 chunk
 #endif
 #ifndef QZ_ABSMEAN_BLOCKS
-#define QZ_ABSMEAN_BLOCKS 2048  // tuning knob: target stage-1 workgroups
+#define QZ_ABSMEAN_BLOCKS 1024  // tuning knob: target stage-1 workgroups
 #endif
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
   // >= QZ_ABSMEAN_MIN_TC tokens per chunk (32 per wave: one round of 8 loads); about
@@ -178,31 +219,34 @@ int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
 }
 
 #ifndef QZ_WMEAN_BLOCKS
-#define QZ_WMEAN_BLOCKS 1024  // tuning knob: target stage-1 workgroups of w_mean
+#define QZ_WMEAN_BLOCKS 256  // tuning knob: target stage-1 workgroups of w_mean
 #endif
-// row chunks of the w_mean stage 1: >= 16 rows each (4 per wave), about QZ_WMEAN_BLOCKS workgroups
+#ifndef QZ_WMEAN_MIN_RC
+#define QZ_WMEAN_MIN_RC 16  // tuning knob: minimum rows per stage-1 chunk
+#endif
+// row chunks of the w_mean stage 1: >= QZ_WMEAN_MIN_RC rows each, about QZ_WMEAN_BLOCKS workgroups
 int64_t wmean_chunks(int64_t R, int64_t C, int64_t* rc) {
   const int64_t bx = cdiv(C, 512);
-  const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, 16), cdiv(QZ_WMEAN_BLOCKS, bx)));
+  const int64_t nrc = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, QZ_WMEAN_MIN_RC), cdiv(QZ_WMEAN_BLOCKS, bx)));
   *rc = cdiv(R, nrc);
   return cdiv(R, *rc);
 }
 
 // ------------------------------------------------- a4: w_mean numerator (f64 sums)
-// stage 1: block = 4 waves over one 512-column window x a chunk of rows; lane owns 8 columns;
-// the 4 wave sums are added in a fixed order -> part[row chunk][c].  Stage 2 (k_colsum_final)
-// adds the chunks in a fixed order: deterministic, like the activation means.
+// stage 1: the stats_rows walk above over the weight rows (a group of L = g/8 lanes is inside one
+// 512-column window, so lanes whose columns were clamped form whole groups and only compute
+// discarded sums); per row the group absmax by DPP, then |w| / bf16(absmax + 1e-6) in bf16,
+// summed in f64 -> part[row chunk][c].  Stage 2 (k_colsum_final) adds the chunks in order.
 template <int LOGL>
-__global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t rc,
-                                                  double* part) {
+__global__ __launch_bounds__(WWP * 64) void k_wmean_v8(const uint16_t* w, int64_t R, int64_t C, int64_t ld, int64_t rc,
+                                                       double* part) {
   constexpr int L = 1 << LOGL;
-  __shared__ double red[4][512];
+  __shared__ double red[WWP][512];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * 512 + lane * 8;
-  const bool in = c0 < C;  // uniform per group of L lanes (C % group == 0)
+  const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * 512 + lane * 8, C - 8);
   const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto row = [&](const uint4 v) {
+  stats_rows<WWP, QZ_WMEAN_NB>(w + c0, ld, r0, r1, wv, [&](const uint4 v) {
     const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
     // group absmax on |bf16| bit patterns (v_pk_max_u16 + DPP), then |w| / bf16(amax + 1e-6)
     const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
@@ -214,23 +258,8 @@ __global__ __launch_bounds__(256) void k_wmean_v8(const uint16_t* w, int64_t R, 
       acc[2 * k] += (double)bfr(__uint_as_float(u[k] << 16) * rd);
       acc[2 * k + 1] += (double)bfr(__uint_as_float(u[k] & 0xffff0000u) * rd);
     }
-  };
-  int64_t r = r0 + wv;
-  for (; r + 12 < r1; r += 16) {  // 4 rows in flight per lane
-    uint4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[j] = in ? *reinterpret_cast<const uint4*>(w + (r + 4 * j) * ld + c0) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) row(v[j]);
-  }
-  for (; r < r1; r += 4) row(in ? *reinterpret_cast<const uint4*>(w + r * ld + c0) : make_uint4(0, 0, 0, 0));
-#pragma unroll
-  for (int i = 0; i < 8; ++i) red[wv][lane * 8 + i] = acc[i];
-  __syncthreads();
-  for (int j = threadIdx.x; j < 512; j += 256) {
-    const int64_t c = (int64_t)blockIdx.x * 512 + j;
-    if (c < C) part[(int64_t)blockIdx.y * C + c] = ((red[0][j] + red[1][j]) + red[2][j]) + red[3][j];
-  }
+  });
+  stats_block_sum<WWP>(red, acc, lane, wv, C, part + (int64_t)blockIdx.y * C);
 }
 // generic: one thread per column walks every row in order (deterministic); any group size /
 // alignment
@@ -355,10 +384,11 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   int64_t tc;
   const int64_t nch = absmean_chunks(tokens, channels, &tc);
   float* part = (float*)workspace;
-  const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16);
+  const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16) &&
+                  tokens < INT32_MAX && ld < INT32_MAX;
   if (v8) {
     dim3 grid((unsigned)cdiv(channels, 512), (unsigned)nch);
-    hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(256), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
+    hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(AWP * 64), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
   } else {
     dim3 grid((unsigned)cdiv(channels, 256), (unsigned)nch);
     hipLaunchKernelGGL(k_absmean_partial_v1, grid, dim3(256), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
@@ -406,7 +436,7 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
   hipStream_t st = (hipStream_t)stream;
   const int64_t g = group_size;
   const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;
-  if (pow2 && ld % 8 == 0 && aligned(w, 16)) {
+  if (pow2 && ld % 8 == 0 && aligned(w, 16) && rows < INT32_MAX && ld < INT32_MAX) {
     if (!workspace || workspace_bytes < qz_awq_weight_mean_workspace_size(rows, cols, group_size))
       return QZ_ERR_WORKSPACE;
     if (!aligned(workspace, 8)) return QZ_ERR_ALIGN;
@@ -418,13 +448,13 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
     const uint16_t* wp = (const uint16_t*)w;
     double* part = (double*)workspace;
     switch (logl) {
-      case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      case 1: hipLaunchKernelGGL(k_wmean_v8<1>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      case 2: hipLaunchKernelGGL(k_wmean_v8<2>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      case 3: hipLaunchKernelGGL(k_wmean_v8<3>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      case 4: hipLaunchKernelGGL(k_wmean_v8<4>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      case 5: hipLaunchKernelGGL(k_wmean_v8<5>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
-      default: hipLaunchKernelGGL(k_wmean_v8<6>, grid, dim3(256), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 1: hipLaunchKernelGGL(k_wmean_v8<1>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 2: hipLaunchKernelGGL(k_wmean_v8<2>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 3: hipLaunchKernelGGL(k_wmean_v8<3>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 4: hipLaunchKernelGGL(k_wmean_v8<4>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      case 5: hipLaunchKernelGGL(k_wmean_v8<5>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
+      default: hipLaunchKernelGGL(k_wmean_v8<6>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
     }
     int e = launch_err();
     if (e) return e;

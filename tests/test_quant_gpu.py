@@ -272,28 +272,30 @@ def test_awq_stats(cuda):
 
 def _wmean_tree(w: torch.Tensor, g: int) -> torch.Tensor:
     """Fixed-order restatement of qz_awq_weight_mean_accum's reduction tree (one call into a
-    zero wsum): terms bf16(|w| / bf16(group absmax + 1e-6)) (the oracle's elementwise values),
-    summed in f64 exactly as the two kernels do -- per row chunk, wave j sums rows j, j+4, ... in
-    order, chunk = ((s0 + s1) + s2) + s3; then wave v of stage 2 sums chunks v, v+16, ... and the
-    16 wave sums are added in order."""
+    zero wsum; the build's defaults QZ_WMEAN_WPB = 8 waves, QZ_WMEAN_BLOCKS = 256, 16 rows minimum
+    per chunk): terms bf16(|w| / bf16(group absmax + 1e-6)) (the oracle's elementwise values),
+    summed in f64 exactly as the two kernels do -- per row chunk, wave j sums rows j, j+8, ... in
+    order, chunk = (((s0 + s1) + s2) + ...) + s7; then wave v of stage 2 sums chunks v, v+16, ...
+    and the 16 wave sums are added in order."""
     import numpy as np
+    wpb, blocks = 8, 256
     R, C = w.shape
     v = w.reshape(-1, g).abs()
     v = (v / (v.amax(dim=1, keepdim=True) + 1e-6)).reshape(R, C).double().numpy()
     bx = -(-C // 512)
-    nrc = max(1, min(-(-R // 16), -(-1024 // bx)))
+    nrc = max(1, min(-(-R // 16), -(-blocks // bx)))
     rc = -(-R // nrc)
     nch = -(-R // rc)
     part = np.zeros((nch, C))
     for k in range(nch):
         r0, r1 = k * rc, min(R, (k + 1) * rc)
-        ws = []
-        for j in range(4):
+        t = None
+        for j in range(wpb):
             acc = np.zeros(C)
-            for r in range(r0 + j, r1, 4):
+            for r in range(r0 + j, r1, wpb):
                 acc = acc + v[r]
-            ws.append(acc)
-        part[k] = ((ws[0] + ws[1]) + ws[2]) + ws[3]
+            t = acc if t is None else t + acc
+        part[k] = t
     red = []
     for wv in range(16):
         acc = np.zeros(C)
