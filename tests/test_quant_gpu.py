@@ -270,6 +270,32 @@ def test_awq_stats(cuda):
         torch.testing.assert_close(got.cpu(), ct.awq_grid_scales(xm, ref, ratio, True), rtol=2e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("tokens,ch", [(1, 8), (7, 264), (333, 1032), (4099, 520)])
+def test_absmean_ragged_windows(cuda, tokens, ch):
+    """Channel counts that leave a 512-column window partly empty (the stage-1 lanes past the
+    last column load clamped addresses and their sums are discarded) and token counts that
+    leave waves with a partial batch: equal to the oracle's accumulation (f32, order-dependent
+    -> rtol), and the sums outside [0, ch) untouched."""
+    g = torch.Generator().manual_seed(tokens)
+    x = torch.randn(tokens, ch, generator=g).to(torch.bfloat16)
+    sums = torch.full((ch + 16,), 7.0, dtype=torch.float32, device=cuda)
+    n = ops.awq_absmean_accum(x.to(cuda), sums[:ch])
+    assert n == tokens
+    ref, _ = ct.awq_accumulate_mean(x.unsqueeze(0))
+    torch.testing.assert_close(sums[:ch].cpu(), ref + 7.0, rtol=1e-5, atol=1e-4)
+    assert torch.equal(sums[ch:].cpu(), torch.full((16,), 7.0))
+
+
+@pytest.mark.parametrize("rows,cols,g", [(1, 32, 32), (9, 96, 32), (45, 640, 128), (1001, 1088, 64)])
+def test_weight_mean_ragged_windows(cuda, rows, cols, g):
+    """w_mean with a partly empty last column window and row counts that are not multiples of
+    the waves per workgroup: the fixed-order tree, bit for bit."""
+    w = _w(rows, cols, seed=rows)
+    wsum = torch.zeros(cols, dtype=torch.float64, device=cuda)
+    assert ops.awq_weight_mean_accum(w.to(cuda), g, wsum) == rows
+    assert torch.equal(wsum.cpu(), _wmean_tree(w, g))
+
+
 def _wmean_tree(w: torch.Tensor, g: int) -> torch.Tensor:
     """Fixed-order restatement of qz_awq_weight_mean_accum's reduction tree (one call into a
     zero wsum; the build's defaults QZ_WMEAN_WPB = 8 waves, QZ_WMEAN_BLOCKS = 256, 16 rows minimum
