@@ -279,7 +279,7 @@ class _ExpertInputs:
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches: experts outer, grid inner
-OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "1") == "1"  # expert searches: loss kernels on a side stream
+OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "0") == "1"  # expert searches: loss kernels on a side stream (measured slower: off)
 
 
 def _overlapped_losses(hs, ref_out, wq_all, losses) -> None:
