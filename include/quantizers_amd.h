@@ -237,6 +237,20 @@ int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols
                         qz_stream_t stream);
 
 /*
+ * The same loss in two phases, for a search that evaluates many (grid point, expert) losses
+ * before it needs any of them: qz_awq_sq_err_partials writes the per-block f64 partial sums of
+ * one loss into part[0 .. qz_awq_sq_err_partials_count(rows, cols)) (stage 1 of
+ * qz_awq_sq_err_accum), and qz_awq_sq_err_reduce then adds n losses' partial rows (row i at
+ * part + i * part_ld) into out[i] with stage 2's fixed order -- one launch for the whole search;
+ * out[i] is bit-identical to qz_awq_sq_err_accum on the same outputs.
+ */
+int64_t qz_awq_sq_err_partials_count(int64_t rows, int64_t cols);
+int qz_awq_sq_err_partials(const void* a, const void* b, int64_t rows, int64_t cols, int64_t lda,
+                           int64_t ldb, double* part, qz_stream_t stream);
+int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part_ld, double* out,
+                         qz_stream_t stream);
+
+/*
  * qz_awq_grid_scales -- one grid point of [3P] AWQModifier._compute_best_scale (fp32):
  * s = clamp(x_mean^r / (w_mean^(1-r) + 1e-4), 1e-4) (duo) or clamp(x_mean^r, 1e-4);
  * s /= sqrt(max(s) * min(s)); inf/nan -> 1.  Single workgroup; channels <= 65536.

@@ -30,7 +30,7 @@ EXPORTS = (
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
-    "qz_grouped_blocks",
+    "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
 )
 
 
@@ -82,6 +82,9 @@ def load() -> ctypes.CDLL:
         "qz_awq_grid_scales_batched": ([P, P, I64, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "qz_awq_sq_err_workspace_size": ([I64, I64], SZ),
         "qz_awq_sq_err_accum": ([P, P, I64, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
+        "qz_awq_sq_err_partials_count": ([I64, I64], I64),
+        "qz_awq_sq_err_partials": ([P, P, I64, I64, I64, I64, P, P], ctypes.c_int),
+        "qz_awq_sq_err_reduce": ([P, I64, I64, I64, P, P], ctypes.c_int),
         "qz_awq_fake_quant_batched": ([P, I64, I64, I64, I64, I64, A, P, I64, P, P, SZ, P], ctypes.c_int),
         "qz_scale_columns": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
         "qz_scale_rows": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),

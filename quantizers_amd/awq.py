@@ -279,7 +279,24 @@ class _ExpertInputs:
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches: experts outer, grid inner
+BATCHED_LOSS = os.environ.get("QZ_BATCHED_LOSS", "1") == "1"  # expert searches: one ordered reduce per search
 OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "0") == "1"  # expert searches: loss kernels on a side stream (measured slower: off)
+
+
+def _batched_losses(hs, ref_out, wq_all, losses) -> None:
+    """Expert-major grid losses with stage 1 only per (expert, grid point) -- the partial sums go
+    to their own row of one [experts, grid, nb] f64 buffer -- and ONE ordered reduce launch for
+    the whole search (qz_awq_sq_err_reduce): a launch and ~5 us of latency-bound stage 2 fewer per
+    loss, the same fixed-order sums, so the same bits as awq_sq_err_accum per loss."""
+    n_grid, n_exp = wq_all.shape[0], len(hs)
+    nb = ops.awq_sq_err_partials_count(ref_out[0].shape)
+    part = torch.empty(n_exp, n_grid, nb, dtype=torch.float64, device=wq_all.device)
+    for k, (h, ro) in enumerate(zip(hs, ref_out)):
+        for g in range(n_grid):
+            ops.awq_sq_err_partials(ro, nn.functional.linear(h, wq_all[g, k]), part[k, g])
+    tot = torch.zeros(n_exp, n_grid, dtype=torch.float64, device=wq_all.device)
+    ops.awq_sq_err_reduce(part.view(n_exp * n_grid, nb), nb, tot)
+    losses += tot.t()
 
 
 def _overlapped_losses(hs, ref_out, wq_all, losses) -> None:
@@ -798,6 +815,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                 ops.fake_quantize_batched(w0, a, scales[g], out=wq_all[g])
             if OVERLAP_LOSS and w0.is_cuda:
                 _overlapped_losses(hs, ref_out, wq_all, losses)
+            elif BATCHED_LOSS and w0.is_cuda and all(ro.shape == ref_out[0].shape for ro in ref_out):
+                _batched_losses(hs, ref_out, wq_all, losses)
             else:
                 for k, (h, ro) in enumerate(zip(hs, ref_out)):
                     for g in range(n_grid):

@@ -189,7 +189,10 @@ __global__ __launch_bounds__(256) void k_sqdiff_partial(const uint16_t* a, const
 }
 // stage 2: one workgroup (4 waves) sums the partials in a fixed order (thread t: t, t+256, ...;
 // then wave sums; then the 4 wave sums in order) and accumulates into *out
-__global__ __launch_bounds__(256) void k_sqdiff_final(const double* part, int64_t nb, double* out) {
+// blockIdx.x = loss i of a batched reduce: partial row part + i * part_ld -> out[i]
+__global__ __launch_bounds__(256) void k_sqdiff_final(const double* part, int64_t nb, int64_t part_ld, double* out) {
+  part += (int64_t)blockIdx.x * part_ld;
+  out += blockIdx.x;
   double acc = 0.0;
 #pragma unroll 4
   for (int64_t k = threadIdx.x; k < nb; k += 256) acc += part[k];
@@ -418,7 +421,33 @@ int qz_awq_sq_err_accum(const void* a, const void* b, int64_t rows, int64_t cols
                      rows, cols, lda, ldb, v8, (double*)workspace);
   int rc = launch_err();
   if (rc) return rc;
-  hipLaunchKernelGGL(k_sqdiff_final, dim3(1), dim3(256), 0, st, (const double*)workspace, nb, out);
+  hipLaunchKernelGGL(k_sqdiff_final, dim3(1), dim3(256), 0, st, (const double*)workspace, nb, (int64_t)0, out);
+  return launch_err();
+}
+
+int64_t qz_awq_sq_err_partials_count(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return sqdiff_blocks(rows, cols);
+}
+
+int qz_awq_sq_err_partials(const void* a, const void* b, int64_t rows, int64_t cols, int64_t lda, int64_t ldb,
+                           double* part, qz_stream_t stream) {
+  if (!a || !b || !part) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || lda < cols || ldb < cols) return QZ_ERR_SHAPE;
+  if (!aligned(part, 8)) return QZ_ERR_ALIGN;
+  const int64_t nb = sqdiff_blocks(rows, cols);
+  const int v8 = lda == cols && ldb == cols && cols % 8 == 0 && aligned(a, 16) && aligned(b, 16);
+  hipLaunchKernelGGL(k_sqdiff_partial, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)a,
+                     (const uint16_t*)b, rows, cols, lda, ldb, v8, part);
+  return launch_err();
+}
+
+int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part_ld, double* out, qz_stream_t stream) {
+  if (n == 0) return QZ_OK;
+  if (!part || !out) return QZ_ERR_NULL;
+  if (n < 0 || nb <= 0 || part_ld < nb || n > INT32_MAX) return QZ_ERR_SHAPE;
+  if (!aligned(part, 8) || !aligned(out, 8)) return QZ_ERR_ALIGN;
+  hipLaunchKernelGGL(k_sqdiff_final, dim3((unsigned)n), dim3(256), 0, (hipStream_t)stream, part, nb, part_ld, out);
   return launch_err();
 }
 

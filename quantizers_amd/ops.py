@@ -553,6 +553,50 @@ def awq_sq_err_accum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> tor
     return out
 
 
+def awq_sq_err_partials_count(shape) -> int:
+    """Number of f64 partial sums one loss over a bf16 output of ``shape`` writes."""
+    r = 1
+    for d in shape[:-1]:
+        r *= int(d)
+    return int(_lib.load().qz_awq_sq_err_partials_count(r, int(shape[-1])))
+
+
+def awq_sq_err_partials(a: torch.Tensor, b: torch.Tensor, part: torch.Tensor) -> None:
+    """Stage 1 of ``awq_sq_err_accum`` into ``part`` (a float64 device row of at least
+    ``awq_sq_err_partials_count(a.shape)`` entries); reduce later with ``awq_sq_err_reduce``."""
+    _check_dev(a, "a")
+    if a.shape != b.shape or a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16:
+        raise ValueError("awq_sq_err_partials: a and b must be bf16 tensors of the same shape")
+    a2 = a.reshape(-1, a.shape[-1]) if a.dim() != 1 else a.reshape(1, -1)
+    b2 = b.reshape(-1, b.shape[-1]) if b.dim() != 1 else b.reshape(1, -1)
+    if a2.stride(-1) != 1:
+        a2 = a2.contiguous()
+    if b2.stride(-1) != 1:
+        b2 = b2.contiguous()
+    r, c = a2.shape
+    lib = _lib.load()
+    if part.dtype != torch.float64 or not part.is_cuda or part.stride(-1) != 1 or \
+            part.numel() < lib.qz_awq_sq_err_partials_count(r, c):
+        raise ValueError("awq_sq_err_partials: part must be a contiguous float64 device row of "
+                         "awq_sq_err_partials_count(shape) entries")
+    rc = lib.qz_awq_sq_err_partials(_ptr(a2), _ptr(b2), r, c, a2.stride(0), b2.stride(0), _ptr(part), _stream())
+    _lib.check(rc, "qz_awq_sq_err_partials")
+
+
+def awq_sq_err_reduce(part: torch.Tensor, nb: int, out: torch.Tensor) -> torch.Tensor:
+    """out.view(-1)[i] += fixed-order sum of part[i, :nb] for every row i of the 2-D float64
+    ``part`` (one launch; bit-identical to ``awq_sq_err_accum`` per loss)."""
+    if part.dtype != torch.float64 or part.dim() != 2 or part.stride(1) != 1 or not part.is_cuda:
+        raise ValueError("awq_sq_err_reduce: part must be a 2-D float64 device tensor with unit column stride")
+    if out.dtype != torch.float64 or not out.is_contiguous() or out.numel() != part.shape[0]:
+        raise ValueError("awq_sq_err_reduce: out must be a contiguous float64 tensor with one entry per row")
+    if nb > part.shape[1]:
+        raise ValueError("awq_sq_err_reduce: nb exceeds the partial rows")
+    rc = _lib.load().qz_awq_sq_err_reduce(_ptr(part), part.shape[0], int(nb), part.stride(0), _ptr(out), _stream())
+    _lib.check(rc, "qz_awq_sq_err_reduce")
+    return out
+
+
 def awq_grid_scales(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo_scaling: bool,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
     x_mean = x_mean.to(torch.float32).contiguous()

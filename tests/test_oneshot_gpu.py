@@ -511,7 +511,7 @@ def test_moe_fast_eager_experts(cuda, monkeypatch, arch):
         _eq(p1[n], p0[n], n)
 
 
-@pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS"])
+@pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS", "BATCHED_LOSS"])
 def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
     """The expert-search speed knobs (experts-outer order; one GEMM for the per-expert inputs)
     change nothing: loss histories and smoothed parameters equal with the knob on and off."""

@@ -473,6 +473,37 @@ def test_awq_sq_err_accum(cuda, shape, strided):
     assert abs(out.item() - 0.5 - want) <= 1e-12 * max(want, 1.0)
 
 
+def test_awq_sq_err_two_phase_matches_accum(cuda):
+    """qz_awq_sq_err_partials into rows of one buffer + ONE qz_awq_sq_err_reduce == one
+    qz_awq_sq_err_accum per loss, bit for bit (the same fixed-order tree), for several output
+    shapes (each reduce call has one partial count), strided rows, and the out[] accumulation."""
+    g = torch.Generator().manual_seed(5)
+    for shape, strided in (((2048, 768), False), ((333, 100), False), ((512, 768), True), ((1, 8), False)):
+        n = 6
+        pairs = []
+        for _ in range(n):
+            a = torch.randn(*shape, generator=g).to(torch.bfloat16).to(cuda)
+            b = (a.float() + torch.randn(*shape, generator=g).to(cuda) * 0.01).to(torch.bfloat16)
+            if strided:
+                big = torch.zeros(shape[0], shape[1] + 64, dtype=torch.bfloat16, device=cuda)
+                big[:, :shape[1]] = a
+                a = big[:, :shape[1]]
+            pairs.append((a, b))
+        nb = ops.awq_sq_err_partials_count(shape)
+        assert nb >= 1
+        part = torch.full((n, nb + 3), float("nan"), dtype=torch.float64, device=cuda)  # padded rows
+        for i, (a, b) in enumerate(pairs):
+            ops.awq_sq_err_partials(a, b, part[i])
+        got = torch.full((n,), 0.25, dtype=torch.float64, device=cuda)
+        ops.awq_sq_err_reduce(part, nb, got)
+        want = torch.full((n,), 0.25, dtype=torch.float64, device=cuda)
+        for i, (a, b) in enumerate(pairs):
+            ops.awq_sq_err_accum(a, b, want[i:i + 1])
+        assert torch.equal(got.cpu(), want.cpu()), (shape, got, want)
+    with pytest.raises(ValueError):
+        ops.awq_sq_err_reduce(part, nb + 4, got)
+
+
 @pytest.mark.parametrize("scheme", [SCHEMES[i] for i in (0, 3, 11, 15, 17, 18)], ids=_id)
 def test_large_launch_nontemporal_path(cuda, scheme):
     """Launches above 256 MiB take the non-temporal load/store variants (group, tile and NVFP4
