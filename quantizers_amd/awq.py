@@ -51,6 +51,7 @@ from .quantization import QuantizationArgs
 from .recipe import AWQMapping
 
 log = logging.getLogger(__name__)
+_D9_LOGGED: set = set()  # (layer class, balance suffix) pairs already reported at INFO
 
 # llmcompressor's default mappings for Llama/Qwen-style decoder blocks
 DEFAULT_MAPPINGS = [
@@ -116,7 +117,11 @@ def resolve_mappings(layer: nn.Module, prefix: str, mappings: List[AWQMapping],
                     if not re.match(_rx(brx), n[len(sparent) + 1:]):
                         continue
                     if smooth_is_linear and lins[n].weight.shape[1] != width:
-                        log.info("AWQ: dropping balance %s of %s (shape mismatch, D9)", n, sname)
+                        # at INFO once per (layer class, balance suffix): every GQA layer repeats it
+                        key = (type(layer).__name__, n[len(prefix):])
+                        log.log(logging.DEBUG if key in _D9_LOGGED else logging.INFO,
+                                "AWQ: dropping balance %s of %s (shape mismatch, D9)", n, sname)
+                        _D9_LOGGED.add(key)
                         continue
                     balance.append(n)
             if not balance:
