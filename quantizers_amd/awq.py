@@ -36,6 +36,7 @@ per mapping).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import os
 import re
@@ -45,7 +46,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 import torch
 from torch import nn
 
-from . import _lib, ops
+from . import _lib, moe_eager, ops
 from .model import LinearRef, batch_groups, checkpoint_name, is_fused_experts, iter_linears, stacked_view
 from .quantization import QuantizationArgs
 from .recipe import AWQMapping
@@ -730,19 +731,24 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         if any(o is not None for o in obs):
             world, rank = 1, 0  # the observer memory runs through the grid in order: no ratio split
         losses = torch.zeros(n_grid, dtype=torch.float64, device=x_mean.device)
-        for i in range(rank, n_grid, world):
-            ratio = i / n_grid
-            ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
-            for g, w0, t, o in zip(groups, orig, tmp, obs):
-                if o is not None:
-                    _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
-                    _view(g).copy_(t)
-                elif len(g) == 1:
-                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
-                else:
-                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
-                    _view(g).copy_(t)
-            losses[i] = _sq_err(ref_out, run())
+        # balance layers all inside fused experts: the router and the cached inputs are unchanged
+        # by the grid, so the experts' routing is fixed across its forwards (moe_eager.fixed_routing)
+        fixed = r.parent_kind == "module" and all(b.index is not None for b in r.balance)
+        routing = moe_eager.fixed_routing() if fixed else contextlib.nullcontext()
+        with routing:
+            for i in range(rank, n_grid, world):
+                ratio = i / n_grid
+                ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
+                for g, w0, t, o in zip(groups, orig, tmp, obs):
+                    if o is not None:
+                        _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
+                        _view(g).copy_(t)
+                    elif len(g) == 1:
+                        ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
+                    else:
+                        ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
+                        _view(g).copy_(t)
+                losses[i] = _sq_err(ref_out, run())
         for g, w0 in zip(groups, orig):
             _view(g).copy_(w0)
         if world > 1:

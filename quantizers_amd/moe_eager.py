@@ -28,6 +28,7 @@ from torch import nn
 log = logging.getLogger(__name__)
 
 FAST_EAGER = os.environ.get("QZ_FAST_EAGER_EXPERTS", "1") == "1"  # A/B knob: 0 = the eager loop itself
+PLANNED = os.environ.get("QZ_PLANNED_EXPERTS", "1") == "1"  # A/B knob: per-expert GEMMs from a grid's fixed routing
 
 
 def eager_forward(module: nn.Module) -> Optional[Callable]:
@@ -81,10 +82,71 @@ def fast_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Ten
     return final
 
 
+# Routing plans of the active ``fixed_routing`` context: (module, input) -> host expert bounds
+_FIXED: Optional[Dict[Tuple, Dict]] = None
+
+
+@contextlib.contextmanager
+def fixed_routing():
+    """Inside, the experts' routing does not change between forwards: an AWQ grid whose balance
+    layers are all expert weights re-runs the MoE block on the same cached inputs through the
+    same router, so the routing of the first grid forward holds for all of them.  The first
+    forward turns the routing into host-side expert bounds (one host sync per grid) and every
+    forward then runs the per-expert GEMMs from those bounds (``planned_eager``) -- torch's
+    ``grouped_mm`` on ROCm reads its group offsets on the host at every call, which drains the
+    GPU twice per forward."""
+    global _FIXED
+    prev, _FIXED = _FIXED, {}
+    try:
+        yield
+    finally:
+        _FIXED = prev
+
+
+def _plan(m: nn.Module, top_k_index: torch.Tensor) -> Dict:
+    k = top_k_index.shape[1]
+    flat = top_k_index.reshape(-1).to(torch.int64)
+    _, perm = torch.sort(flat, stable=True)  # (token, slot) pairs grouped by expert
+    counts = torch.zeros(m.num_experts, dtype=torch.int64, device=flat.device).scatter_add_(
+        0, flat, torch.ones_like(flat))
+    bounds = [0] + counts.cumsum(0).tolist()  # the one host sync
+    return {"perm": perm, "tok": perm // k, "bounds": bounds, "order": torch.argsort(top_k_index, dim=-1)}
+
+
+def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Tensor,
+                  top_k_weights: torch.Tensor, p: Dict) -> torch.Tensor:
+    """``fast_eager`` with the expert bounds on the host: one GEMM per routed expert over its
+    rows of the expert-sorted tokens (the eager loop's per-expert GEMM shapes), no host sync."""
+    t, k = top_k_index.shape
+    xg = hidden_states[p["tok"]]
+    b = p["bounds"]
+    gu = torch.empty(xg.shape[0], m.gate_up_proj.shape[1], dtype=xg.dtype, device=xg.device)
+    for e in range(m.num_experts):
+        if b[e + 1] > b[e]:
+            torch.mm(xg[b[e]:b[e + 1]], m.gate_up_proj[e].t(), out=gu[b[e]:b[e + 1]])
+    gate, up = gu.chunk(2, dim=-1)
+    h = m.act_fn(gate) * up
+    d = torch.empty(xg.shape[0], m.down_proj.shape[1], dtype=h.dtype, device=h.device)
+    for e in range(m.num_experts):
+        if b[e + 1] > b[e]:
+            torch.mm(h[b[e]:b[e + 1]], m.down_proj[e].t(), out=d[b[e]:b[e + 1]])
+    perm = p["perm"]
+    d = d * top_k_weights.reshape(-1)[perm][:, None]
+    contrib = torch.empty_like(d)
+    contrib[perm] = d
+    contrib = contrib.view(t, k, -1)
+    contrib = torch.gather(contrib, 1, p["order"][:, :, None].expand(-1, -1, contrib.shape[-1]))
+    final = torch.zeros_like(hidden_states)
+    for j in range(k):
+        final = final + contrib[:, j].to(final.dtype)
+    return final
+
+
 class FastEagerExperts:
     """Instance-level forward for one experts module (see the module docstring)."""
 
     checked: Dict[Tuple, bool] = {}  # (class, shape, dtype) -> fast path verified; shared per pass
+    planned_checked: Dict[Tuple, bool] = {}  # the same for planned_eager (checked against fast_eager)
 
     def __init__(self, module: nn.Module, eager: Callable):
         self.m = module
@@ -109,6 +171,22 @@ class FastEagerExperts:
             return want
         if not ok:
             return self.eager(self.m, hidden_states, top_k_index, top_k_weights)
+        if _FIXED is not None and PLANNED:
+            pkey = (id(self.m), hidden_states.data_ptr(), tuple(hidden_states.shape), tuple(top_k_index.shape))
+            plan = _FIXED.get(pkey)
+            if plan is None:
+                plan = _FIXED[pkey] = _plan(self.m, top_k_index)
+            pok = FastEagerExperts.planned_checked.get(key)
+            if pok is None:
+                want = fast_eager(self.m, hidden_states, top_k_index, top_k_weights)
+                pok = _bits_equal(planned_eager(self.m, hidden_states, top_k_index, top_k_weights, plan), want)
+                FastEagerExperts.planned_checked[key] = pok
+                if not pok:
+                    log.info("MoE: per-expert planned form differs for %s at %s; grouped form kept",
+                             type(self.m).__name__, key[1])
+                return want
+            if pok:
+                return planned_eager(self.m, hidden_states, top_k_index, top_k_weights, plan)
         return fast_eager(self.m, hidden_states, top_k_index, top_k_weights)
 
 
@@ -118,6 +196,7 @@ def eager_experts(model: nn.Module):
     (``FastEagerExperts``) inside the context; the modules' own forwards are restored after."""
     patched = []
     FastEagerExperts.checked = {}
+    FastEagerExperts.planned_checked = {}
     try:
         for mod in model.modules():
             fwd = eager_forward(mod)
