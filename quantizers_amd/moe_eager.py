@@ -113,6 +113,35 @@ def _plan(m: nn.Module, top_k_index: torch.Tensor) -> Dict:
     return {"perm": perm, "tok": perm // k, "bounds": bounds, "order": torch.argsort(top_k_index, dim=-1)}
 
 
+EXPERT_STREAMS = int(os.environ.get("QZ_EXPERT_STREAMS", "4"))  # concurrent per-expert GEMM streams
+_streams: Dict[torch.device, list] = {}
+
+
+def _per_expert_mm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, b) -> None:
+    """out[rows of e] = x[rows of e] @ w[e]^T for every routed expert e.  A routed expert's GEMM
+    is small (~2k rows: a few dozen output tiles on a 256-CU part), so the experts are spread
+    round-robin over EXPERT_STREAMS streams to run side by side; each GEMM is the same call on
+    the same operands whichever stream runs it, so the bits do not change."""
+    n = EXPERT_STREAMS if x.is_cuda else 1
+    if n <= 1:
+        for e in range(w.shape[0]):
+            if b[e + 1] > b[e]:
+                torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=out[b[e]:b[e + 1]])
+        return
+    main = torch.cuda.current_stream(x.device)
+    ss = _streams.get(x.device)
+    if ss is None or len(ss) != n:
+        ss = _streams[x.device] = [torch.cuda.Stream(x.device) for _ in range(n)]
+    for s in ss:
+        s.wait_stream(main)
+    for e in range(w.shape[0]):
+        if b[e + 1] > b[e]:
+            with torch.cuda.stream(ss[e % n]):
+                torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=out[b[e]:b[e + 1]])
+    for s in ss:
+        main.wait_stream(s)
+
+
 def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Tensor,
                   top_k_weights: torch.Tensor, p: Dict) -> torch.Tensor:
     """``fast_eager`` with the expert bounds on the host: one GEMM per routed expert over its
@@ -121,15 +150,11 @@ def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.
     xg = hidden_states[p["tok"]]
     b = p["bounds"]
     gu = torch.empty(xg.shape[0], m.gate_up_proj.shape[1], dtype=xg.dtype, device=xg.device)
-    for e in range(m.num_experts):
-        if b[e + 1] > b[e]:
-            torch.mm(xg[b[e]:b[e + 1]], m.gate_up_proj[e].t(), out=gu[b[e]:b[e + 1]])
+    _per_expert_mm(xg, m.gate_up_proj, gu, b)
     gate, up = gu.chunk(2, dim=-1)
     h = m.act_fn(gate) * up
     d = torch.empty(xg.shape[0], m.down_proj.shape[1], dtype=h.dtype, device=h.device)
-    for e in range(m.num_experts):
-        if b[e + 1] > b[e]:
-            torch.mm(h[b[e]:b[e + 1]], m.down_proj[e].t(), out=d[b[e]:b[e + 1]])
+    _per_expert_mm(h, m.down_proj, d, b)
     perm = p["perm"]
     d = d * top_k_weights.reshape(-1)[perm][:, None]
     contrib = torch.empty_like(d)
