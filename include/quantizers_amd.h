@@ -249,6 +249,14 @@ int qz_awq_sq_err_partials(const void* a, const void* b, int64_t rows, int64_t c
                            int64_t ldb, double* part, qz_stream_t stream);
 int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part_ld, double* out,
                          qz_stream_t stream);
+/*
+ * qz_awq_sq_err_partials_multi -- qz_awq_sq_err_partials for 1..8 outputs b[0..n_b) (a HOST array
+ * of device pointers) against one reference a, all dense [rows, cols] bf16 (cols % 8 == 0,
+ * 16-B aligned): output g's partials go to part + g * part_ld, bit-identical to a
+ * qz_awq_sq_err_partials(a, b[g]) call, while a is read once for all of them.
+ */
+int qz_awq_sq_err_partials_multi(const void* a, const void* const* b, int32_t n_b, int64_t rows,
+                                 int64_t cols, double* part, int64_t part_ld, qz_stream_t stream);
 
 /*
  * qz_awq_grid_scales -- one grid point of [3P] AWQModifier._compute_best_scale (fp32):

@@ -31,6 +31,7 @@ EXPORTS = (
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
     "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
+    "qz_awq_sq_err_partials_multi",
 )
 
 
@@ -85,6 +86,7 @@ def load() -> ctypes.CDLL:
         "qz_awq_sq_err_partials_count": ([I64, I64], I64),
         "qz_awq_sq_err_partials": ([P, P, I64, I64, I64, I64, P, P], ctypes.c_int),
         "qz_awq_sq_err_reduce": ([P, I64, I64, I64, P, P], ctypes.c_int),
+        "qz_awq_sq_err_partials_multi": ([P, P, I32, I64, I64, P, I64, P], ctypes.c_int),
         "qz_awq_fake_quant_batched": ([P, I64, I64, I64, I64, I64, A, P, I64, P, P, SZ, P], ctypes.c_int),
         "qz_scale_columns": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
         "qz_scale_rows": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),

@@ -286,6 +286,7 @@ class _ExpertInputs:
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
 EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches: experts outer, grid inner
 BATCHED_LOSS = os.environ.get("QZ_BATCHED_LOSS", "1") == "1"  # expert searches: one ordered reduce per search
+MULTI_LOSS = int(os.environ.get("QZ_MULTI_LOSS", "8"))  # expert searches: grid outputs per loss launch (<= 8)
 OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "0") == "1"  # expert searches: loss kernels on a side stream (measured slower: off)
 
 
@@ -297,7 +298,17 @@ def _batched_losses(hs, ref_out, wq_all, losses) -> None:
     n_grid, n_exp = wq_all.shape[0], len(hs)
     nb = ops.awq_sq_err_partials_count(ref_out[0].shape)
     part = torch.empty(n_exp, n_grid, nb, dtype=torch.float64, device=wq_all.device)
+    multi = MULTI_LOSS if all(ro.is_contiguous() for ro in ref_out) else 1
+    outs = [torch.empty_like(ref_out[0]) for _ in range(multi)] if multi > 1 else []
     for k, (h, ro) in enumerate(zip(hs, ref_out)):
+        if multi > 1:  # up to `multi` grid points' outputs, then one loss launch reading ro once
+            h2 = h.reshape(-1, h.shape[-1])
+            for g0 in range(0, n_grid, multi):
+                gs = range(g0, min(n_grid, g0 + multi))
+                for j, g in enumerate(gs):
+                    torch.mm(h2, wq_all[g, k].t(), out=outs[j].view(-1, outs[j].shape[-1]))
+                ops.awq_sq_err_partials_multi(ro, outs[:len(gs)], part[k, g0:g0 + len(gs)])
+            continue
         for g in range(n_grid):
             ops.awq_sq_err_partials(ro, nn.functional.linear(h, wq_all[g, k]), part[k, g])
     tot = torch.zeros(n_exp, n_grid, dtype=torch.float64, device=wq_all.device)

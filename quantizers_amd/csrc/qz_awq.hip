@@ -202,6 +202,55 @@ __global__ __launch_bounds__(256) void k_sqdiff_final(const double* part, int64_
   __syncthreads();
   if (threadIdx.x == 0) *out += ((red[0] + red[1]) + red[2]) + red[3];
 }
+// stage 1 for up to QZ_SQD_MULTI outputs b[0..G) against ONE shared reference a (dense rows):
+// a unit of a is loaded once for all G outputs; output g is accumulated, reduced and stored
+// exactly as k_sqdiff_partial's v8 path would for (a, b[g]) -> part[g * part_ld + block],
+// so every loss keeps its bits while the reference is read once instead of G times
+constexpr int QZ_SQD_MULTI = 8;
+struct SqdOuts {
+  const uint16_t* p[QZ_SQD_MULTI];
+};
+template <int G>
+__global__ __launch_bounds__(256) void k_sqdiff_partial_multi(const uint16_t* a, SqdOuts B, int64_t n_units,
+                                                              int64_t part_ld, double* part) {
+  double acc[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) acc[g] = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  const uint4* A = reinterpret_cast<const uint4*>(a);
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < n_units; u += stride) {
+    const uint4 x = A[u];
+    const uint32_t xa[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const uint4 y = reinterpret_cast<const uint4*>(B.p[g])[u];
+      const uint32_t ya[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float d0 = bfr(__uint_as_float(xa[k] << 16) - __uint_as_float(ya[k] << 16));
+        const float d1 = bfr(__uint_as_float(xa[k] & 0xffff0000u) - __uint_as_float(ya[k] & 0xffff0000u));
+        acc[g] += (double)(d0 * d0);
+        acc[g] += (double)(d1 * d1);
+      }
+    }
+  }
+  __shared__ double red[G][256 / WAVE];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const double v = warp_sum_f64(acc[g]);
+    if ((threadIdx.x & (WAVE - 1)) == 0) red[g][threadIdx.x / WAVE] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < G) {
+    const int g = threadIdx.x;
+    part[(int64_t)g * part_ld + blockIdx.x] = red[g][0] + red[g][1] + red[g][2] + red[g][3];
+  }
+}
+template <int G>
+void launch_sqd_multi(const uint16_t* a, const SqdOuts& B, int64_t n_units, int64_t nb, int64_t part_ld, double* part,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(k_sqdiff_partial_multi<G>, dim3((unsigned)nb), dim3(256), 0, st, a, B, n_units, part_ld, part);
+}
 int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
   return std::max<int64_t>(1, std::min<int64_t>(2048, cdiv(rows * cols, 256 * 8 * 4)));
 }
@@ -439,6 +488,35 @@ int qz_awq_sq_err_partials(const void* a, const void* b, int64_t rows, int64_t c
   const int v8 = lda == cols && ldb == cols && cols % 8 == 0 && aligned(a, 16) && aligned(b, 16);
   hipLaunchKernelGGL(k_sqdiff_partial, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const uint16_t*)a,
                      (const uint16_t*)b, rows, cols, lda, ldb, v8, part);
+  return launch_err();
+}
+
+int qz_awq_sq_err_partials_multi(const void* a, const void* const* b, int32_t n_b, int64_t rows, int64_t cols,
+                                 double* part, int64_t part_ld, qz_stream_t stream) {
+  if (!a || !b || !part) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || cols % 8 || n_b < 1 || n_b > QZ_SQD_MULTI) return QZ_ERR_SHAPE;
+  const int64_t nb = sqdiff_blocks(rows, cols);
+  if (part_ld < nb) return QZ_ERR_SHAPE;
+  if (!aligned(part, 8) || !aligned(a, 16)) return QZ_ERR_ALIGN;
+  SqdOuts B = {};
+  for (int g = 0; g < n_b; ++g) {
+    if (!b[g]) return QZ_ERR_NULL;
+    if (!aligned(b[g], 16)) return QZ_ERR_ALIGN;
+    B.p[g] = (const uint16_t*)b[g];
+  }
+  const uint16_t* ap = (const uint16_t*)a;
+  const int64_t n = rows * cols / 8;
+  hipStream_t st = (hipStream_t)stream;
+  switch (n_b) {
+    case 1: launch_sqd_multi<1>(ap, B, n, nb, part_ld, part, st); break;
+    case 2: launch_sqd_multi<2>(ap, B, n, nb, part_ld, part, st); break;
+    case 3: launch_sqd_multi<3>(ap, B, n, nb, part_ld, part, st); break;
+    case 4: launch_sqd_multi<4>(ap, B, n, nb, part_ld, part, st); break;
+    case 5: launch_sqd_multi<5>(ap, B, n, nb, part_ld, part, st); break;
+    case 6: launch_sqd_multi<6>(ap, B, n, nb, part_ld, part, st); break;
+    case 7: launch_sqd_multi<7>(ap, B, n, nb, part_ld, part, st); break;
+    default: launch_sqd_multi<8>(ap, B, n, nb, part_ld, part, st); break;
+  }
   return launch_err();
 }
 

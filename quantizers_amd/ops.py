@@ -583,6 +583,30 @@ def awq_sq_err_partials(a: torch.Tensor, b: torch.Tensor, part: torch.Tensor) ->
     _lib.check(rc, "qz_awq_sq_err_partials")
 
 
+def awq_sq_err_partials_multi(a: torch.Tensor, bs: Sequence[torch.Tensor], part: torch.Tensor) -> None:
+    """``awq_sq_err_partials(a, b)`` for up to 8 outputs ``bs`` against one reference ``a`` in one
+    launch (``a`` read once): output g's partials go to row g of the 2-D float64 ``part``;
+    bit-identical per output.  All tensors dense bf16 of one shape."""
+    _check_dev(a, "a")
+    if not 1 <= len(bs) <= 8:
+        raise ValueError("awq_sq_err_partials_multi: 1 to 8 outputs")
+    for b in bs:
+        if b.shape != a.shape or b.dtype != torch.bfloat16 or not b.is_contiguous():
+            raise ValueError("awq_sq_err_partials_multi: outputs must be contiguous bf16 tensors of a's shape")
+    if a.dtype != torch.bfloat16 or not a.is_contiguous():
+        raise ValueError("awq_sq_err_partials_multi: a must be a contiguous bf16 tensor")
+    if part.dtype != torch.float64 or part.dim() != 2 or part.stride(1) != 1 or part.shape[0] < len(bs):
+        raise ValueError("awq_sq_err_partials_multi: part must be a 2-D float64 tensor with a row per output")
+    c = a.shape[-1]
+    r = a.numel() // c
+    lib = _lib.load()
+    if part.shape[1] < lib.qz_awq_sq_err_partials_count(r, c):
+        raise ValueError("awq_sq_err_partials_multi: part rows shorter than awq_sq_err_partials_count(shape)")
+    ptrs = (ctypes.c_void_p * len(bs))(*[b.data_ptr() for b in bs])
+    rc = lib.qz_awq_sq_err_partials_multi(_ptr(a), ptrs, len(bs), r, c, _ptr(part), part.stride(0), _stream())
+    _lib.check(rc, "qz_awq_sq_err_partials_multi")
+
+
 def awq_sq_err_reduce(part: torch.Tensor, nb: int, out: torch.Tensor) -> torch.Tensor:
     """out.view(-1)[i] += fixed-order sum of part[i, :nb] for every row i of the 2-D float64
     ``part`` (one launch; bit-identical to ``awq_sq_err_accum`` per loss)."""

@@ -511,14 +511,16 @@ def test_moe_fast_eager_experts(cuda, monkeypatch, arch):
         _eq(p1[n], p0[n], n)
 
 
-@pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS", "BATCHED_LOSS", "moe_eager.PLANNED", "moe_eager.EXPERT_STREAMS"])
+@pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS", "BATCHED_LOSS", "moe_eager.PLANNED", "moe_eager.EXPERT_STREAMS",
+                                  "MULTI_LOSS"])
 def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
     """The expert-search speed knobs (experts-outer order; one GEMM for the per-expert inputs)
     change nothing: loss histories and smoothed parameters equal with the knob on and off."""
     import quantizers_amd.awq as awq_mod
     import quantizers_amd.moe_eager as moe_mod
     target, name = (moe_mod, knob.split(".", 1)[1]) if knob.startswith("moe_eager.") else (awq_mod, knob)
-    values = {"EXPERT_STREAMS": {True: 4, False: 1}}.get(name, {True: True, False: False})
+    values = {"EXPERT_STREAMS": {True: 4, False: 1}, "MULTI_LOSS": {True: 8, False: 1}}.get(
+        name, {True: True, False: False})
     out = {}
     for on in (True, False):
         monkeypatch.setattr(target, name, values[on])

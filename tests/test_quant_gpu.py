@@ -504,6 +504,26 @@ def test_awq_sq_err_two_phase_matches_accum(cuda):
         ops.awq_sq_err_reduce(part, nb + 4, got)
 
 
+@pytest.mark.parametrize("n_b", [1, 3, 8])
+def test_awq_sq_err_partials_multi_matches_single(cuda, n_b):
+    """One launch over n_b outputs sharing a reference == n_b single-output partial launches, bit
+    for bit (rows of the partial table, then the reduced losses)."""
+    g = torch.Generator(device=cuda).manual_seed(n_b)
+    shape = (1000, 264)
+    a = torch.randn(*shape, device=cuda, generator=g).to(torch.bfloat16)
+    bs = [(a.float() + torch.randn(*shape, device=cuda, generator=g) * 0.01).to(torch.bfloat16) for _ in range(n_b)]
+    nb = ops.awq_sq_err_partials_count(shape)
+    got = torch.full((n_b, nb + 2), float("nan"), dtype=torch.float64, device=cuda)
+    want = torch.full_like(got, float("nan"))
+    ops.awq_sq_err_partials_multi(a, bs, got)
+    for i, b in enumerate(bs):
+        ops.awq_sq_err_partials(a, b, want[i])
+    assert torch.equal(got[:, :nb].cpu(), want[:, :nb].cpu())
+    assert torch.isnan(got[:, nb:]).all()  # nothing written past the partial count
+    with pytest.raises(ValueError):
+        ops.awq_sq_err_partials_multi(a, bs * 9, got)
+
+
 @pytest.mark.parametrize("scheme", [SCHEMES[i] for i in (0, 3, 11, 15, 17, 18)], ids=_id)
 def test_large_launch_nontemporal_path(cuda, scheme):
     """Launches above 256 MiB take the non-temporal load/store variants (group, tile and NVFP4
