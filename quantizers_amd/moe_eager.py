@@ -110,7 +110,14 @@ def _plan(m: nn.Module, top_k_index: torch.Tensor) -> Dict:
     counts = torch.zeros(m.num_experts, dtype=torch.int64, device=flat.device).scatter_add_(
         0, flat, torch.ones_like(flat))
     bounds = [0] + counts.cumsum(0).tolist()  # the one host sync
-    return {"perm": perm, "tok": perm // k, "bounds": bounds, "order": torch.argsort(top_k_index, dim=-1)}
+    # row of the expert-sorted output that lands in (token t, j-th expert in ascending id): the
+    # scatter back to (token, slot) order and the gather into ascending-expert order composed
+    # into ONE index, so the forward moves the [t * k, H] contributions once instead of twice
+    order = torch.argsort(top_k_index, dim=-1)
+    inv = torch.argsort(perm)
+    base = torch.arange(top_k_index.shape[0], device=flat.device)[:, None] * k
+    src = inv[(base + order).reshape(-1)]
+    return {"perm": perm, "tok": perm // k, "bounds": bounds, "src": src}
 
 
 EXPERT_STREAMS = int(os.environ.get("QZ_EXPERT_STREAMS", "4"))  # concurrent per-expert GEMM streams
@@ -155,12 +162,8 @@ def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.
     h = m.act_fn(gate) * up
     d = torch.empty(xg.shape[0], m.down_proj.shape[1], dtype=h.dtype, device=h.device)
     _per_expert_mm(h, m.down_proj, d, b)
-    perm = p["perm"]
-    d = d * top_k_weights.reshape(-1)[perm][:, None]
-    contrib = torch.empty_like(d)
-    contrib[perm] = d
-    contrib = contrib.view(t, k, -1)
-    contrib = torch.gather(contrib, 1, p["order"][:, :, None].expand(-1, -1, contrib.shape[-1]))
+    d = d * top_k_weights.reshape(-1)[p["perm"]][:, None]
+    contrib = d.index_select(0, p["src"]).view(t, k, -1)
     final = torch.zeros_like(hidden_states)
     for j in range(k):
         final = final + contrib[:, j].to(final.dtype)
