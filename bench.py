@@ -19,10 +19,18 @@ rocprofv3 kernel trace of the same command is summarised by scripts/prof_summary
 
 Beside it (not the headline): the north-star synthetic weight [11008, 4096] (grouped and one
 launch per weight), the AWQ kernels, a 2-layer AWQ oneshot, the other BASELINE configs, and the
-CPU baseline (the oracle's torch restatement on the host cores).  Multi-GPU: one process per GPU
-(torchrun), each quantizes its own model-sized weight set (weak scaling, no collective in the
-timed region); afterwards the ranks reassemble the compressed tensors with bucketed RCCL
-all-gathers (``distributed.gather_state``), timed separately.
+CPU baseline (the oracle's torch restatement on the host cores).
+
+Multi-GPU: one process per GPU.  ``--gpus N`` under torchrun (WORLD_SIZE=N) runs as rank
+RANK; ``--gpus N`` without a torchrun environment starts the N ranks itself (a
+``torch.distributed.run`` child process; this process never touches the GPU), and a mismatch
+between ``--gpus`` and WORLD_SIZE is an error, so ``n_gpus`` is always the ranks that ran
+(``ranks_seen`` = the process group's size).  The headline is weak scaling: each rank
+compresses its own Qwen3-4B-sized weight set (no collective in the timed region).  Beside it,
+at every N: the row-sharded synthetic leg ([11008, 4096] split into N row
+blocks, kernel-only and end-to-end including the RCCL all-gather of the packed codes and
+scales) and the strong-scaling leg (ONE Qwen3-4B sharded over the ranks by the product's
+plan, plus ``distributed.gather_state``'s all-gather of the compressed state dict).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -69,11 +77,14 @@ def kernel_name(grouped: bool, launch_weight_bytes: int, logl: int = 4, kind: in
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); without a torchrun environment bench.py starts them itself")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--copies", type=int, default=12)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--launch-check", action="store_true",
+                   help="start the ranks, join the process group, print the rank census and exit (no GPU use)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extras", action="store_true", help="headline only (no secondary legs)")
     p.add_argument("--profile-only", action="store_true",
@@ -83,10 +94,12 @@ def parse():
 
 def cpu_baseline(seconds: float, checks=None):
     """The oracle's torch restatement of compressed-tensors (oracle/ct_torch.py), timed on the host
-    cores on a bounded sample of the headline workload: repeated compress_weight calls on one
-    Qwen3-4B gate_proj-shaped weight [9728, 2560] (the model's largest shape class).  The oracle
-    is used only here (the CPU leg) and as the checker of ``checks`` = [(input rows, packed
-    codes, scales)] taken from the GPU's measured outputs (plain-C restatement, bit for bit).
+    cores on a bounded sample of the headline workload: repeated compress_weight calls on the
+    north-star synthetic weight [11008, 4096] (seed 0, N(0, 0.02^2) bf16), one
+    warm-up call, then at least 5 timed calls for about ``seconds``; best and median per call
+    reported, ``value`` = the median.  The oracle is used only here (the CPU leg) and as the
+    checker of ``checks`` = [(input rows, packed codes, scales)] taken from the GPU's measured
+    outputs (plain-C restatement, bit for bit).
 
     Threads: 16 = the GPU box's CPU share for one GPU (its OMP_NUM_THREADS; gpurun sizes one
     GPU's host share at 16 of the node's os.cpu_count() cores), not os.cpu_count() as BASELINE.md
@@ -102,23 +115,25 @@ def cpu_baseline(seconds: float, checks=None):
             ok = ok and bool(torch.equal(codes, ref_p) and torch.equal(scale.view(torch.int16), ref_s.view(torch.int16)))
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    rows, cols = 9728, 2560
     g = torch.Generator().manual_seed(0)
-    w = (torch.randn(rows, cols, generator=g) * 0.02).to(torch.bfloat16)
+    w = (torch.randn(ROWS, COLS, generator=g) * 0.02).to(torch.bfloat16)
     a = ct.QArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
     ct.compress_weight(w, a)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 5 or (time.perf_counter() - t_start < seconds and len(times) < 200):
+        t0 = time.perf_counter()
         ct.compress_weight(w, a)
-        n += 1
-        el = time.perf_counter() - t0
-        if (el >= seconds and n >= 3) or n >= 2000:
-            break
-    res = {"value": n * rows * cols / el, "unit": "params/s", "cores": threads, "kind": "port",
+        times.append(time.perf_counter() - t0)
+    times.sort()
+    med = times[len(times) // 2]
+    res = {"value": PARAMS / med, "unit": "params/s", "cores": threads, "kind": "port",
+           "best_params_per_s": PARAMS / times[0], "median_s_per_call": med, "best_s_per_call": times[0],
+           "calls": len(times),
            "sample": f"oracle/ct_torch.compress_weight (compressed-tensors op sequence, torch CPU) int4-g{GROUP} on "
-                     f"one Qwen3-4B gate_proj-shaped bf16 weight [{rows},{cols}], {n} calls in {el:.1f}s, torch "
-                     f"threads={threads} (the box's per-GPU CPU share), os.cpu_count()={os.cpu_count()}, "
-                     f"cpu='{cpu_model()}'"}
+                     f"the north-star synthetic bf16 weight [{ROWS},{COLS}] (seed 0, N(0, 0.02^2)): 1 warm-up + "
+                     f"{len(times)} timed calls in {sum(times):.1f}s, value = median call, torch threads={threads} "
+                     f"(the box's per-GPU CPU share), os.cpu_count()={os.cpu_count()}, cpu='{cpu_model()}'"}
     return res, ok
 
 
@@ -245,7 +260,7 @@ def _all_gather_into(out, inp):
     if dist.get_backend() == "gloo":
         parts = [torch.empty_like(inp, device="cpu") for _ in range(dist.get_world_size())]
         dist.all_gather(parts, inp.cpu())
-        out.copy_(torch.stack(parts))
+        out.copy_(torch.cat([p.reshape(-1) for p in parts]).view_as(out))
     else:
         dist.all_gather_into_tensor(out, inp)
 
@@ -367,17 +382,251 @@ def synthetic_leg(ops, QuantizationArgs, dev, gen, stream, copies_n, k):
     return res, copies, check
 
 
+def row_blocks(rows: int, world: int, align: int = 8):
+    """BASELINE.md §2's multi-GPU split of one weight: ``world`` contiguous row blocks of equal
+    height (a multiple of ``align`` rows, so an asymmetric zero point packed along dim 0 stays
+    word-aligned), the last ones possibly short or empty: [(r0, r1)] per rank, and the padded
+    block height every rank's all-gather slot has."""
+    blk = -(-rows // world)
+    blk = -(-blk // align) * align
+    return [(min(r * blk, rows), min((r + 1) * blk, rows)) for r in range(world)], blk
+
+
+def row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank, reps=5):
+    """BASELINE.md §2 multi-GPU row: the north-star synthetic weight [11008, 4096] int4-g128 split
+    into ``world`` row blocks (``row_blocks``), rank r quantizing block r (strong scaling: the
+    weight is fixed).  Every rank generates the same copies (seeded), keeps only its block.
+
+    * kernel-only: ONE grouped launch over ``n`` distinct copies of the rank's block (n x block
+      bytes >= 1 GB, beyond the 256 MiB Infinity Cache), HIP events on the launch stream, median
+      of ``reps``; aggregate params/s = 11008 x 4096 / (max over ranks of the time per copy);
+    * end-to-end: per copy, the rank's block quantized (one launch) and the packed codes and
+      scales reassembled on EVERY rank by ``all_gather_into_tensor`` into the full
+      [11008, 512] int32 / [11008, 32] bf16 tensors (RCCL over xGMI); wall clock between
+      barriers, max over ranks;
+    * check: the gathered tensors of copy 0 equal one single-GPU quantize of the whole copy 0,
+      bit for bit (rank 0)."""
+    a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, strategy="group", group_size=GROUP)
+    blocks, blk = row_blocks(ROWS, world)
+    r0, r1 = blocks[rank]
+    mine = r1 - r0
+    blk_bytes = max(blk, 8) * COLS * 2
+    n = max(4, min(128, -(-(1 << 30) // blk_bytes)))
+    copies = []
+    for i in range(n):
+        g = torch.Generator(device=dev).manual_seed(5000 + i)
+        full = (torch.randn(ROWS, COLS, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        copies.append(full[r0:r1].clone() if mine else None)
+        del full
+    res = {"split": f"{world} row blocks of {blk} rows (rank {rank}: rows {r0}-{r1})", "copies": n,
+           "weight": f"[{ROWS}, {COLS}] int4 sym g{GROUP}"}
+    # kernel-only: one grouped launch over the n copies of this rank's block
+    us_copy = 0.0
+    if mine:
+        outs = [ops.alloc_outputs((mine, COLS), a, None, dev) for _ in range(n)]
+        gq = ops.GroupedQuantize(copies, a, outs=outs)
+        for _ in range(3):
+            gq.run(stream)
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            gq.run(stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / n)
+        us_copy = sorted(ts)[len(ts) // 2]
+        del gq, outs
+    t = torch.tensor([us_copy], device=dev, dtype=torch.float64)
+    if world > 1:
+        _all_reduce_max(t)
+    us_max = t.item()
+    alg_rank = mine * COLS * 2.515625
+    res["kernel_only"] = {"us_per_copy_max_rank": us_max, "us_per_copy_this_rank": us_copy,
+                          "params_per_s": PARAMS / (us_max * 1e-6),
+                          "per_gpu_GBps": alg_rank / (us_copy * 1e-6) / 1e9 if us_copy else None,
+                          "per_gpu_frac": alg_rank / (us_copy * 1e-6) / 1e9 / HBM_PEAK_GBS if us_copy else None,
+                          "per_gpu_read_frac": mine * COLS * 2 / (us_copy * 1e-6) / 1e9 / HBM_PEAK_GBS
+                          if us_copy else None,
+                          "how": "one grouped launch over the copies of this rank's block, HIP events, median"}
+    # end to end: quantize the block, all-gather codes + scales into the full tensors
+    codes_blk = torch.zeros(blk, COLS // 8, dtype=torch.int32, device=dev)
+    scale_blk = torch.zeros(blk, COLS // GROUP, dtype=torch.bfloat16, device=dev)
+    codes_full = torch.empty(world * blk, COLS // 8, dtype=torch.int32, device=dev)
+    scale_full = torch.empty(world * blk, COLS // GROUP, dtype=torch.bfloat16, device=dev)
+    prep = ops.PreparedQuantize(copies[0], a, {"codes": codes_blk[:mine], "scale": scale_blk[:mine]}) \
+        if mine else None
+
+    def one(i):
+        if prep is not None:
+            prep.run(copies[i % n], stream)
+        if world > 1:
+            _all_gather_into(codes_full, codes_blk)
+            _all_gather_into(scale_full, scale_blk)
+
+    for i in range(3):
+        one(i)
+    k = min(n, 32)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(k):
+        one(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / k], device=dev, dtype=torch.float64)
+    if world > 1:
+        _all_reduce_max(t)
+    e2e = t.item()
+    res["end_to_end"] = {"us_per_copy": e2e * 1e6, "params_per_s": PARAMS / e2e,
+                         "gathered_bytes_per_copy": world * blk * (COLS // 8 * 4 + COLS // GROUP * 2),
+                         "how": "per copy: the block's quantize launch + all_gather_into_tensor of the packed codes "
+                                "and the scales into the full tensors on every rank; wall clock between barriers, "
+                                "max over ranks" + ("" if world > 1 else " (1 rank: nothing to gather)")}
+    # bit-exact check of the reassembled copy 0 against one whole-weight quantize
+    one(0)
+    torch.cuda.synchronize()
+    ok = None
+    if rank == 0:
+        g = torch.Generator(device=dev).manual_seed(5000)
+        full = (torch.randn(ROWS, COLS, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        ref = ops.quantize_weight(full, a)
+        got_c = codes_full[:ROWS] if world > 1 else codes_blk[:ROWS]
+        got_s = scale_full[:ROWS] if world > 1 else scale_blk[:ROWS]
+        ok = bool(torch.equal(ref["codes"], got_c) and torch.equal(ref["scale"].view(torch.int16),
+                                                                    got_s.view(torch.int16)))
+        del full, ref
+    res["gathered_equals_single_gpu"] = ok
+    del copies, codes_full, scale_full, prep
+    torch.cuda.empty_cache()
+    return res
+
+
+def strong_model_leg(units, dev, stream, world, rank, steps=10):
+    """The product's sharded whole-model compression (strong scaling: ONE Qwen3-4B, its 252
+    linears assigned to ranks by ``distributed.plan_shards`` -- LPT on bytes, as
+    ``compressed_state_dict`` does -- each rank running its share as grouped launches), then the
+    compressed state dict reassembled on every rank by ``distributed.gather_state`` (one RCCL
+    ``all_gather_into_tensor`` into the result buffer).
+
+    * kernel-only: HIP events around ``steps`` runs of the rank's share, max over ranks;
+    * end-to-end: ``steps`` x (the share's launches + ``gather_state``), wall clock between
+      barriers, max over ranks."""
+    from quantizers_amd.compressor import CompressionPlan
+    from quantizers_amd.distributed import gather_state, plan_shards
+    shards = plan_shards([(str(i), u.nbytes) for i, u in enumerate(units)], world)
+    mine = [units[int(i)] for i in shards[rank]]
+    total = sum(u.nbytes // 2 for u in units)
+    plan = CompressionPlan(mine, dev) if mine else None
+    res = {"model_params": total, "units_total": len(units), "units_this_rank": len(mine),
+           "params_this_rank": plan.params if plan else 0, "launches_this_rank": plan.launches if plan else 0}
+    ms = 0.0
+    if plan is not None:
+        for _ in range(3):
+            plan.run(stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(steps):
+            plan.run(stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / steps
+    t = torch.tensor([ms], device=dev, dtype=torch.float64)
+    if world > 1:
+        _all_reduce_max(t)
+    res["kernel_only"] = {"ms_max_rank": t.item(), "ms_this_rank": ms, "params_per_s": total / (t.item() * 1e-3),
+                          "how": "HIP events around the rank's share (grouped launches), max over ranks"}
+    local = plan.tensors() if plan is not None else {}
+    local = {k: v for k, v in local.items() if v.is_cuda}  # weight_shape stays on the host
+    nbytes = sum(v.numel() * v.element_size() for v in local.values())
+
+    def one():
+        if plan is not None:
+            plan.run(stream)
+        return gather_state(local)  # RCCL: device buffers; gloo rehearsal: through the host
+
+    got = one()
+    n_got = len(got)
+    del got
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        got = one()
+        del got
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([(time.perf_counter() - t0) / steps], device=dev, dtype=torch.float64)
+    if world > 1:
+        _all_reduce_max(t)
+    res["end_to_end"] = {"ms": t.item() * 1e3, "params_per_s": total / t.item(), "tensors_on_every_rank": n_got,
+                         "compressed_bytes_this_rank": nbytes,
+                         "how": "per step: the rank's share + distributed.gather_state (all_gather_into_tensor of "
+                                "every rank's flat compressed bytes into the result buffer on every rank); wall clock "
+                                "between barriers, max over ranks"}
+    del plan, local
+    torch.cuda.empty_cache()
+    return res
+
+
+def _spawn_ranks(n: int) -> int:
+    """``--gpus N`` outside a torchrun environment: run N rank processes of this script under
+    ``torch.distributed.run`` as a CHILD process (this process never initialises the GPU and
+    never execs) and return their exit status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def launch_check(world, rank, backend):
+    """``--launch-check``: join the process group, census the ranks, print one JSON line on rank
+    0 and exit -- the rank plumbing of ``--gpus N`` without touching a GPU (CPU-testable)."""
+    dist.init_process_group("gloo")
+    seen = [None] * dist.get_world_size()
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                  "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_seen": dist.get_world_size(),
+                          "ranks": seen, "backend_for_run": backend}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        sys.exit(_spawn_ranks(args.gpus))  # the ranks print the line; nothing here touches the GPU
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report an n_gpus the run "
+              f"does not have", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # QZ_BENCH_BACKEND=gloo: rehearsal of the multi-rank code path on a box with fewer GPUs than
     # ranks (ranks share devices, collectives go through host memory); the driver's N-GPU runs
     # use the default RCCL ("nccl") backend, one rank per GPU.
     backend = os.environ.get("QZ_BENCH_BACKEND", "nccl")
+    if args.launch_check:
+        launch_check(world, rank, backend)
+        return
+    n_dev = torch.cuda.device_count()  # counts devices without initialising the GPU
     if backend == "gloo":
-        local = local % max(torch.cuda.device_count(), 1)
+        local = local % max(n_dev, 1)
+    elif world > 1 and n_dev < world:
+        print(f"bench.py: {world} ranks need {world} GPUs for RCCL, {n_dev} visible "
+              f"(QZ_BENCH_BACKEND=gloo rehearses the ranks on fewer)", file=sys.stderr)
+        sys.exit(2)
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -446,22 +695,11 @@ def main():
             w = part[0][1]
             checks.append((w[:64].cpu(), gq.outs[0]["codes"][:64].cpu(), gq.outs[0]["scale"][:64].cpu()))
 
-    # reassembly across ranks (north star: RCCL all-gather over xGMI), outside the timing
-    allgather = None
-    if world > 1:
-        from quantizers_amd.distributed import gather_state
-        local_t = plan.tensors()
-        nbytes = sum(t.numel() * t.element_size() for t in local_t.values())
-        gather_state({f"r{rank}.{k}": v for k, v in local_t.items()})  # warm (communicator, buffers)
-        torch.cuda.synchronize()
-        dist.barrier()
-        ta = time.perf_counter()
-        got = gather_state({f"r{rank}.{k}": v for k, v in local_t.items()})
-        torch.cuda.synchronize()
-        dist.barrier()
-        allgather = {"ms": (time.perf_counter() - ta) * 1e3, "bytes_per_rank": nbytes,
-                     "tensors_gathered": len(got), "how": "distributed.gather_state: bucketed all_gather_into_tensor"}
-        del got, local_t
+    # multi-GPU legs (BASELINE.md §2 multi-GPU row; north star: RCCL all-gather over xGMI), run at
+    # every N so the driver's 1/2/4/8-GPU lines carry comparable fields
+    ranks_seen = dist.get_world_size() if world > 1 else 1
+    strong = strong_model_leg(units, dev, stream, world, rank, steps=10 if backend == "nccl" else 2)
+    row_sharded = row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank)
     # PCIe-inclusive rate (not the headline): what save_compressed pays per model on one GPU --
     # the same plan, then every output tensor copied to pinned host memory (_HostCopier: side
     # stream, one device->host copy per tensor).  One warm run first (pinned-host allocator).
@@ -521,7 +759,8 @@ def main():
             pmc = json.load(open(pmc_path))
             if pmc.get("alg_bytes_per_step") == alg_step and pmc.get("launches_per_step") == launches_step:
                 traffic = pmc["hbm_bytes_per_launch"]
-                traffic_src = (f"profiles/headline_pmc.json ({pmc['tag']}): FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                traffic_src = (f"committed PMC passes, not re-read in this run: profiles/headline_pmc.json "
+                               f"({pmc['tag']}), FETCH_SIZE x2 + WRITE_SIZE per launch of this same plan, "
                                f"{pmc['traffic_over_algorithmic']:.4f} x algorithmic")
         line = {
             "metric": METRIC,
@@ -555,7 +794,9 @@ def main():
             "per_launch": per_launch,
             "cpu_baseline": cpu,
             "parity_check": ok,
-            "allgather": allgather,
+            "ranks_seen": ranks_seen,
+            "row_sharded_synthetic_11008x4096": row_sharded,
+            "strong_scaling_qwen3_4b_sharded": strong,
             "pcie_inclusive": pcie,
         }
         line.update(extras)

@@ -204,9 +204,14 @@ int qz_pack_int32(const int8_t* v, int64_t rows, int64_t cols, int32_t num_bits,
  * qz_awq_absmean_accum -- adds sum_t |x[t, c]| (fp32, decision D8) into sum[c] for a bf16
  * activation block x [tokens, channels] (row stride ld).  Replaces the running mean|x| of
  * [3P] llmcompressor AWQModifier's cache_smooth_activations_hook (_accumulate_mean).
- * Deterministic: fixed-order two-stage reduction through `workspace`
- * (qz_awq_absmean_workspace_size bytes).
+ * Deterministic: fixed-order reduction through `workspace` (qz_awq_absmean_workspace_size
+ * bytes), in ONE launch: the last-arriving workgroup of each column window sums the window's
+ * row-chunk partials.  Statistics workspace contract (absmean and w_mean): its first
+ * QZ_STATS_HEAD_BYTES bytes are arrival counters that must be zero before the first call on that
+ * workspace (e.g. one hipMemset when it is allocated); every call leaves them zero again.  Do
+ * not share a statistics workspace with other entry points or between concurrent streams.
  */
+#define QZ_STATS_HEAD_BYTES 32768
 size_t qz_awq_absmean_workspace_size(int64_t tokens, int64_t channels);
 int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_t ld,
                          float* sum, void* workspace, size_t workspace_bytes,
@@ -216,13 +221,23 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
  * qz_awq_weight_mean_accum -- adds sum_r |W[r,c]| / (absmax(group(r,c)) + 1e-6) (bf16
  * elementwise, fp64 sum) into wsum[c] for one balance layer W [rows, cols].  group_size =
  * the layer's quantization group (cols for channel strategy).  Replaces [3P] llmcompressor
- * _compute_layer_means.  Deterministic: fixed-order two-stage reduction through `workspace`
- * (qz_awq_weight_mean_workspace_size bytes, 8-B aligned; may be 0 bytes for the generic path).
+ * _compute_layer_means.  Deterministic: fixed-order reduction through `workspace`
+ * (qz_awq_weight_mean_workspace_size bytes, 8-B aligned; may be 0 bytes for the generic path),
+ * one launch for power-of-two groups of 8..512 (the statistics workspace contract above).
  */
 size_t qz_awq_weight_mean_workspace_size(int64_t rows, int64_t cols, int32_t group_size);
 int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld,
                              int32_t group_size, double* wsum, void* workspace,
                              size_t workspace_bytes, qz_stream_t stream);
+
+/*
+ * qz_awq_stats_layout -- the reduction plan the statistics calls use for a [rows, cols] input
+ * (which = 0: absmean, rows = tokens; 1: w_mean with group_size): out[0] one-launch (1) or
+ * two-launch (0), out[1] column window, out[2] rows per chunk, out[3] chunks, out[4] row slots
+ * per workgroup, out[5] final-sum thread groups, out[6] counter head bytes.  Lets a caller (or a
+ * test) restate the fixed summation order exactly.  No reference counterpart.
+ */
+int qz_awq_stats_layout(int32_t which, int64_t rows, int64_t cols, int32_t group_size, int64_t* out);
 
 /*
  * qz_awq_sq_err_accum -- the grid search's loss numerator: *out += sum over [rows, cols] of

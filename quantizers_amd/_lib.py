@@ -31,7 +31,7 @@ EXPORTS = (
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
     "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
-    "qz_awq_sq_err_partials_multi",
+    "qz_awq_sq_err_partials_multi", "qz_awq_stats_layout",
 )
 
 
@@ -78,6 +78,7 @@ def load() -> ctypes.CDLL:
         "qz_awq_absmean_accum": ([P, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
         "qz_awq_weight_mean_workspace_size": ([I64, I64, I32], SZ),
         "qz_awq_weight_mean_accum": ([P, I64, I64, I64, I32, P, P, SZ, P], ctypes.c_int),
+        "qz_awq_stats_layout": ([I32, I64, I64, I32, P], ctypes.c_int),
         "qz_awq_grid_scales": ([P, P, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "qz_awq_fake_quant": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),
         "qz_awq_grid_scales_batched": ([P, P, I64, I64, ctypes.c_float, I32, P, P], ctypes.c_int),

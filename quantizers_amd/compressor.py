@@ -453,26 +453,120 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
     return out
 
 
-def _order_key(units: Sequence[CompressUnit], raw: Dict[str, torch.Tensor]):
-    """Checkpoint tensor order (and so the shard split): compression units in model order, names
-    sorted within a unit, then the unchanged tensors by name -- the same whether the tensors come
-    from one process chunk by chunk or from the ranks' all-gather."""
-    unit_of = {r.name: i for i, u in enumerate(units) for r in u.refs}
-    last = len(units)
+def _unit_layout(u: CompressUnit) -> List[Tuple[str, int]]:
+    """Names and byte sizes of a unit's on-disk tensors, known before anything runs (the
+    shapes ``ops._compressed_tensors`` gives each module, per expert for a stacked unit)."""
+    a = u.scheme.weights
+    int_q, _ = ops._compress_plan(a, u.scheme.input_activations is not None)
+    rows, cols = (int(x) for x in u.refs[0].weight.shape[-2:])
+    gshape = ops.n_groups(a, rows, cols)
+    ng = 1
+    for d in gshape:
+        ng *= d
+    scale_b = ng * torch.empty((), dtype=ops._scale_dtype(a)).element_size()
+    sizes: Dict[str, int] = {}
+    if a.type == "int":
+        pf = 32 // a.num_bits
+        if int_q:
+            sizes["weight"] = rows * cols
+        else:
+            sizes["weight_packed"] = rows * ((cols + pf - 1) // pf) * 4
+            sizes["weight_shape"] = 2 * 8
+        sizes["weight_scale"] = scale_b
+        if not a.symmetric and a.strategy in ("group", "channel"):
+            sizes["weight_zero_point"] = ng if int_q else (gshape[0] + pf - 1) // pf * gshape[1] * 4
+    elif a.num_bits == 8:
+        sizes["weight"] = rows * cols
+        sizes["weight_scale"] = scale_b
+    else:
+        sizes["weight_packed"] = rows * cols // 2
+        sizes["weight_scale"] = scale_b
+        if a.is_nvfp4:
+            sizes["weight_global_scale"] = 4
+    return [(f"{r.name}.{k}", nb) for r in u.refs for k, nb in sizes.items()]
 
-    def key(name: str):
-        if name in raw:
-            return (last, name)
-        return (unit_of.get(name.rsplit(".", 1)[0], last), name)
-    return key
+
+def _split_shards(items: Sequence[Tuple[str, int]], max_shard_bytes: int) -> List[List[str]]:
+    """The shard split of ``items`` (checkpoint order): a shard closes when the next tensor would
+    take it past ``max_shard_bytes`` (a tensor larger than that is a shard of its own)."""
+    shards: List[List[str]] = [[]]
+    size = 0
+    for n, nb in items:
+        if shards[-1] and size + nb > max_shard_bytes:
+            shards.append([])
+            size = 0
+        shards[-1].append(n)
+        size += nb
+    return shards
+
+
+@dataclass
+class SavePlan:
+    """Who writes what, computed identically on every rank before anything is compressed.
+
+    ``order``: every checkpoint tensor (name, bytes) in checkpoint order -- compression units in
+    model order, names sorted within a unit, then the unchanged tensors by name; ``shards``: the
+    split of that order into files (``files``); ``owner[s]``: the rank that writes shard ``s``
+    (contiguous runs of shards, balanced by bytes); ``units_of[r]`` / ``raw_of[r]``: the units
+    rank ``r`` compresses and the unchanged tensors it writes -- exactly those with a tensor in
+    one of its shards (a unit straddling two ranks' shards is compressed by both)."""
+
+    order: List[Tuple[str, int]]
+    shards: List[List[str]]
+    files: List[str]
+    owner: List[int]
+    units_of: List[List[int]]
+    raw_of: List[List[str]]
+
+    @property
+    def total_bytes(self) -> int:
+        return sum(nb for _, nb in self.order)
+
+    def weight_map(self) -> Dict[str, str]:
+        return {n: f for names, f in zip(self.shards, self.files) for n in names}
+
+
+def save_plan(units: Sequence[CompressUnit], raw: Dict[str, torch.Tensor], world: int,
+              max_shard_bytes: int = SHARD_BYTES) -> SavePlan:
+    order: List[Tuple[str, int]] = []
+    unit_of: Dict[str, int] = {}
+    for i, u in enumerate(units):
+        lay = sorted(_unit_layout(u))
+        order.extend(lay)
+        for n, _ in lay:
+            unit_of[n] = i
+    order.extend(sorted((k, v.numel() * v.element_size()) for k, v in raw.items()))
+    shards = _split_shards(order, max_shard_bytes)
+    n = len(shards)
+    files = ["model.safetensors"] if n == 1 else [f"model-{i + 1:05d}-of-{n:05d}.safetensors" for i in range(n)]
+    size = dict(order)
+    total = max(1, sum(size.values()))
+    owner, before = [], 0
+    for names in shards:  # rank of a shard = where its byte midpoint falls: contiguous, balanced
+        nb = sum(size[x] for x in names)
+        owner.append(min(world - 1, int(world * (before + nb / 2) / total)))
+        before += nb
+    units_of: List[set] = [set() for _ in range(world)]
+    raw_of: List[List[str]] = [[] for _ in range(world)]
+    for names, r in zip(shards, owner):
+        for x in names:
+            if x in unit_of:
+                units_of[r].add(unit_of[x])
+            else:
+                raw_of[r].append(x)
+    return SavePlan(order, shards, files, owner, [sorted(s) for s in units_of], raw_of)
 
 
 def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SHARD_BYTES, device=None) -> str:
-    """Write safetensors shards + index + config.json(quantization_config).  One process: the
-    shards stream out while the next plans compress (a shard is handed to a writer thread as
-    soon as its bytes are on the host).  Under ``torch.distributed`` the compression is sharded
-    over the ranks (``compressed_state_dict``) and rank 0 alone writes; every rank returns after
-    the files exist."""
+    """Write safetensors shards + index + config.json(quantization_config).
+
+    The shard split is fixed up front from the tensors' names and sizes (``save_plan``: the same
+    files, byte for byte, whatever the number of ranks).  One process writes every shard; under
+    ``torch.distributed`` (one process per GPU) each rank compresses only the units whose
+    tensors fall in ITS shards, copies them device -> host over its own PCIe link and writes
+    those files itself -- no compressed byte crosses xGMI or funnels through rank 0; rank 0 adds
+    the index and config.  Either way a shard is handed to a writer thread as soon as its bytes
+    are on the host, while later plans compress.  Every rank returns after all files exist."""
     world, rank = _dist_info()
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     qcfg = quantization_config(model)
@@ -481,94 +575,95 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
         model.config.quantization_config = qcfg
     t0 = time.perf_counter()
     units, raw = compression_units(model)
-    key = _order_key(units, raw)
-    n_tensors, n_bytes = 0, 0
-    if world == 1 and device.type == "cuda":
-        writer = _ShardWriter(output_dir, max_shard_bytes)
-        copier = _HostCopier(device)
-        tm: Dict[str, float] = {}
-        for t in _compress_chunks(units, device, copier, tm):
-            writer.add(sorted(t.items(), key=lambda kv: key(kv[0])), copier.last_event)
-        host_raw, _ = _raw_to_host(raw, device, copier)  # same copier stream: its last event covers all
-        writer.add(sorted(host_raw.items()), copier.last_event)
-        n_tensors, n_bytes = writer.close()
+    plan = save_plan(units, raw, world, max_shard_bytes)
+    mine = [units[i] for i in plan.units_of[rank]]
+    my_raw = {k: raw[k] for k in plan.raw_of[rank]}
+    writer = _PlannedShardWriter(output_dir, plan, rank)
+    copier = _HostCopier(device) if device.type == "cuda" else None
+    tm: Dict[str, float] = {}
+    for t in _compress_chunks(mine, device, copier, tm):
+        writer.add(t, copier.last_event if copier is not None else None)
+    host_raw, rc = _raw_to_host(my_raw, device, copier)  # same copier stream: its last event covers all
+    writer.add(host_raw, copier.last_event if copier is not None else (rc.last_event if rc is not None else None))
+    n_tensors, n_bytes = writer.close()
+    if copier is not None:
         copier.finish()
-        log.info("compressed_state_dict phases (s): %s", tm)
-    else:
-        sd = compressed_state_dict(model, device, dst=0)
-        if rank == 0:
-            writer = _ShardWriter(output_dir, max_shard_bytes)
-            writer.add(sorted(sd.items(), key=lambda kv: key(kv[0])))
-            n_tensors, n_bytes = writer.close()
+    if rc is not None and rc is not copier:
+        rc.finish()
+    log.info("save_compressed rank %d/%d: %d shard(s), %d tensors, %.2f GB; phases (s): %s", rank, world,
+             plan.owner.count(rank), n_tensors, n_bytes / 1e9, tm)
     if rank == 0:
+        if len(plan.files) > 1:
+            with open(os.path.join(output_dir, "model.safetensors.index.json"), "w") as f:
+                json.dump({"metadata": {"total_size": plan.total_bytes},
+                           "weight_map": dict(sorted(plan.weight_map().items()))}, f, indent=2)
         _write_config(model, qcfg, output_dir)
-        log.info("save_compressed: %d tensors, %.2f GB in %.2fs", n_tensors, n_bytes / 1e9, time.perf_counter() - t0)
+        log.info("save_compressed: %d files, %.2f GB in %.2fs", len(plan.files), plan.total_bytes / 1e9,
+                 time.perf_counter() - t0)
     if world > 1:
         dist.barrier()
     return output_dir
 
 
-def _write_shard_file(shard: Dict[str, torch.Tensor], path: str, ready) -> None:
-    if ready is not None:
-        ready.synchronize()  # the shard's device -> host copies have landed
-    save_file({k: v.contiguous() for k, v in shard.items()}, path, metadata={"format": "pt"})
+class _PlannedShardWriter:
+    """Writes this rank's shards of a ``SavePlan``: tensors arrive in any grouping (plan by plan,
+    then the unchanged ones); a shard is handed to a pool thread (WRITE_THREADS) once all its
+    tensors are here, under its final file name.  Tensors of other ranks' shards are dropped
+    (the halves of a straddling unit); a tensor whose size differs from the plan is an error."""
 
-
-class _ShardWriter:
-    """safetensors shards of at most ``max_shard_bytes`` in the order tensors are added, each
-    written by a pool thread (WRITE_THREADS) once complete; ``close`` names them
-    ``model.safetensors`` (one shard) or ``model-XXXXX-of-NNNNN.safetensors`` + index."""
-
-    def __init__(self, output_dir: str, max_shard_bytes: int):
+    def __init__(self, output_dir: str, plan: SavePlan, rank: int):
         from concurrent.futures import ThreadPoolExecutor
         os.makedirs(output_dir, exist_ok=True)
-        self.dir, self.max = output_dir, max_shard_bytes
-        self.cur: Dict[str, torch.Tensor] = {}
-        self.size = 0
+        self.dir, self.plan = output_dir, plan
+        self.size = dict(plan.order)
+        self.mine = [s for s, r in enumerate(plan.owner) if r == rank]
+        self.shard_of = {n: s for s in self.mine for n in plan.shards[s]}
+        self.missing = {s: len(plan.shards[s]) for s in self.mine}
+        self.held: Dict[int, Dict[str, torch.Tensor]] = {s: {} for s in self.mine}
         self.ready = None
-        self.shards: List[Tuple[str, Dict[str, int]]] = []
         self.pool = ThreadPoolExecutor(max_workers=max(1, WRITE_THREADS))
         self.futures = []
+        self.count = self.bytes = 0
 
-    def add(self, items, ready=None) -> None:
+    def add(self, items: Dict[str, torch.Tensor], ready=None) -> None:
         if ready is not None:
-            self.ready = ready  # one stream: the latest copy event covers every earlier copy
-        for n, t in items:
+            self.ready = ready  # one copy stream: the latest event covers every earlier copy
+        for n, t in items.items():
+            s = self.shard_of.get(n)
+            if s is None or n in self.held[s]:
+                continue
             nb = t.numel() * t.element_size()
-            if self.cur and self.size + nb > self.max:
-                self._flush()
-            self.cur[n] = t
-            self.size += nb
-
-    def _flush(self) -> None:
-        path = os.path.join(self.dir, f".qz-shard-{len(self.shards):05d}.tmp")
-        self.shards.append((path, {n: t.numel() * t.element_size() for n, t in self.cur.items()}))
-        self.futures.append(self.pool.submit(_write_shard_file, self.cur, path, self.ready))
-        self.cur, self.size = {}, 0
+            if nb != self.size[n]:
+                raise ValueError(f"save plan: {n} has {nb} bytes, the plan expected {self.size[n]}")
+            self.held[s][n] = t
+            self.missing[s] -= 1
+            if self.missing[s] == 0:
+                shard = {x: self.held[s][x] for x in self.plan.shards[s]}  # checkpoint order
+                self.held[s] = {}
+                self.count += len(shard)
+                self.bytes += sum(self.size[x] for x in shard)
+                path = os.path.join(self.dir, self.plan.files[s])
+                self.futures.append(self.pool.submit(_write_shard_file, shard, path, self.ready))
 
     def close(self) -> Tuple[int, int]:
-        if self.cur or not self.shards:
-            self._flush()
         try:
             for f in self.futures:
                 f.result()
         finally:
             self.pool.shutdown()
-        n = len(self.shards)
-        total = sum(nb for _, names in self.shards for nb in names.values())
-        count = sum(len(names) for _, names in self.shards)
-        if n == 1:
-            os.replace(self.shards[0][0], os.path.join(self.dir, "model.safetensors"))
-            return count, total
-        wmap = {}
-        for i, (path, names) in enumerate(self.shards):
-            fn = f"model-{i + 1:05d}-of-{n:05d}.safetensors"
-            os.replace(path, os.path.join(self.dir, fn))
-            for nm in names:
-                wmap[nm] = fn
-        with open(os.path.join(self.dir, "model.safetensors.index.json"), "w") as f:
-            json.dump({"metadata": {"total_size": total}, "weight_map": dict(sorted(wmap.items()))}, f, indent=2)
-        return count, total
+        left = {self.plan.files[s]: n for s, n in self.missing.items() if n}
+        if left:
+            raise RuntimeError(f"save plan: shards never completed (tensors missing): {left}")
+        return self.count, self.bytes
+
+
+def _write_shard_file(shard: Dict[str, torch.Tensor], path: str, ready) -> None:
+    if ready is not None:
+        ready.synchronize()  # the shard's device -> host copies have landed
+    tmp = os.path.join(os.path.dirname(path), "." + os.path.basename(path) + ".tmp")
+    save_file({k: (v.cpu() if v.is_cuda else v).contiguous() for k, v in shard.items()}, tmp,
+              metadata={"format": "pt"})
+    os.replace(tmp, path)
 
 
 def _write_config(model: nn.Module, qcfg: dict, output_dir: str) -> None:

@@ -144,6 +144,180 @@ __global__ __launch_bounds__(FW * 64) void k_colsum_final(const T* part, int64_t
   }
 }
 
+// ---------------------------------------------- a3 / a4 in ONE launch (round 3)
+// Narrow column windows (WIN = 128 columns, or the group width when wider): a wave-load covers
+// RPW = 64 / (WIN / 8) rows of WIN columns (lane = 8 columns, 16-B loads, 256-B row segments), so
+// a [rows, C] matrix splits into 4x more windows than with 512-column windows and the row chunks
+// can be 4x fewer for the same number of workgroups: the partial slab is small enough for the
+// LAST-ARRIVING workgroup of each window to reduce it inside the same launch (no second kernel,
+// no launch gap).  Arrival counters live at the head of the caller's workspace (STATS_CNT words,
+// zero before the first call; the last arriver resets its word, so every call leaves them zero).
+// Fixed order, hence deterministic: slot s = wave * RPW + (lane / (WIN / 8)) sums rows
+// r0 + s, r0 + s + S, ... (S = SWP * RPW slots) in order; a chunk's partial is
+// ((slot 0 + slot 1) + ...) + slot S-1; the final sum per column is, over TF = NT / WIN thread
+// groups f, ((sum_f=0 + sum_f=1) + ...) where sum_f adds chunks f, f + TF, ... in order.
+constexpr int STATS_CNT = 8192;  // arrival counters (uint32) at the head of a statistics workspace
+constexpr int64_t STATS_HEAD = (int64_t)STATS_CNT * 4;
+static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics workspace (quantizers_amd.h)");
+#ifndef QZ_STATS_1L
+#define QZ_STATS_1L 1  // 1: one-launch statistics; 0: the two-launch kernels above (A/B knob)
+#endif
+#ifndef QZ_ABS1_WPB
+#define QZ_ABS1_WPB 8
+#endif
+#ifndef QZ_ABS1_NB
+#define QZ_ABS1_NB 8
+#endif
+#ifndef QZ_ABS1_BLOCKS
+#define QZ_ABS1_BLOCKS 1024  // tuning knob: target workgroups of the one-launch absmean
+#endif
+#ifndef QZ_ABS1_MIN_RC
+#define QZ_ABS1_MIN_RC 256  // tuning knob: minimum tokens per chunk
+#endif
+#ifndef QZ_WM1_WPB
+#define QZ_WM1_WPB 8
+#endif
+#ifndef QZ_WM1_NB
+#define QZ_WM1_NB 4
+#endif
+#ifndef QZ_WM1_BLOCKS
+#define QZ_WM1_BLOCKS 512  // tuning knob: target workgroups of the one-launch w_mean
+#endif
+#ifndef QZ_WM1_MIN_RC
+#define QZ_WM1_MIN_RC 128  // tuning knob: minimum rows per chunk
+#endif
+
+// rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per
+// batch, the next batch loaded before the current one is used; f(v, valid) per row in order.  rb
+// is wave-uniform; the loop condition guarantees every row of a non-final batch is valid.
+template <int S, int SNB, typename F>
+__device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int64_t rb, int q, int64_t r1, F&& f) {
+  if (rb >= r1) return;
+  const uint32_t rlast = (uint32_t)(r1 - 1), uld = (uint32_t)ld;
+  auto ld16 = [&](int64_t r) {
+    return *reinterpret_cast<const uint4*>(base + (uint64_t)std::min((uint32_t)r, rlast) * uld);
+  };
+  uint4 cur[SNB];
+#pragma unroll
+  for (int j = 0; j < SNB; ++j) cur[j] = ld16(rb + q + (int64_t)j * S);
+  for (; rb + (int64_t)SNB * S < r1; rb += (int64_t)SNB * S) {
+    uint4 nxt[SNB];
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) nxt[j] = ld16(rb + q + (int64_t)(SNB + j) * S);
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) f(cur[j], true);
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) cur[j] = nxt[j];
+  }
+#pragma unroll
+  for (int j = 0; j < SNB; ++j) f(cur[j], rb + q + (int64_t)j * S < r1);
+}
+
+// combine the slots of this workgroup into part[chunk][c], then the window's last arriver sums
+// the chunks into sum[c] (see the order above) and resets the window's counter
+template <int WIN, int SWP, typename T>
+__device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int lane, int wv, int64_t C, int64_t nch,
+                                             T* part, unsigned* cnt, T* sum) {
+  constexpr int LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, NT = SWP * 64, TF = NT / WIN;
+  static_assert(TF >= 1 && NT % WIN == 0 && S >= TF, "stats window");
+  const int q = lane / LPR, c8 = lane % LPR;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[wv * RPW + q][c8 * 8 + i] = acc[i];
+  __syncthreads();
+  const int64_t cb = (int64_t)blockIdx.x * WIN;
+  for (int j = threadIdx.x; j < WIN; j += NT) {
+    const int64_t c = cb + j;
+    if (c < C) {
+      T t = red[0][j];
+#pragma unroll
+      for (int k = 1; k < S; ++k) t += red[k][j];
+      part[(int64_t)blockIdx.y * C + c] = t;
+    }
+  }
+  __shared__ int last;
+  __threadfence();  // release this workgroup's partials at device scope before it arrives
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const int j = threadIdx.x % WIN, f = threadIdx.x / WIN;
+  const int64_t c = cb + j;
+  T t = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int64_t k = f; k < nch; k += TF)  // coherent device-scope loads: partials of every XCD
+      t += __hip_atomic_load(part + k * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  red[f][j] = t;  // red is free again: every thread passed the barriers above
+  __syncthreads();
+  if (f == 0 && c < C) {
+    T u = red[0][j];
+#pragma unroll
+    for (int k = 1; k < TF; ++k) u += red[k][j];
+    sum[c] += u;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int WIN>
+__global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                                                int64_t tc, int64_t nch, float* part, unsigned* cnt,
+                                                                float* sum) {
+  constexpr int SWP = QZ_ABS1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW;
+  __shared__ float red[S][WIN];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane / LPR;
+  const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
+  const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  stats_walk<S, QZ_ABS1_NB>(x + c0, ld, t0 + wv * RPW, q, t1, [&](const uint4 v, bool ok) {
+    const uint32_t w[4] = {ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += fabsf(__uint_as_float(w[k] << 16));
+      acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
+    }
+  });
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, part, cnt, sum);
+}
+
+template <int WIN, int LOGL>
+__global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w, int64_t R, int64_t C, int64_t ld,
+                                                             int64_t rc, int64_t nch, double* part, unsigned* cnt,
+                                                             double* wsum) {
+  constexpr int SWP = QZ_WM1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, L = 1 << LOGL;
+  static_assert(L <= LPR, "a group must lie inside one row segment of the window");
+  __shared__ double red[S][WIN];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane / LPR;
+  const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
+  const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  stats_walk<S, QZ_WM1_NB>(w + c0, ld, r0 + wv * RPW, q, r1, [&](const uint4 v, bool ok) {
+    const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
+    // group absmax on |bf16| bit patterns (v_pk_max_u16 + DPP, every lane of the group on the same
+    // row, so the group is uniformly valid or not), then |w| / bf16(amax + 1e-6)
+    const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
+    const float m = __uint_as_float(grp_max_u<L>(max(pm & 0xffffu, pm >> 16)) << 16);
+    const float rd = ok ? __builtin_amdgcn_rcpf(bfr(m + 1e-6f)) : 0.f;  // rcp lemma; 0: adds +0.0
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[2 * k] += (double)bfr(__uint_as_float(u[k] << 16) * rd);
+      acc[2 * k + 1] += (double)bfr(__uint_as_float(u[k] & 0xffff0000u) * rd);
+    }
+  });
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, part, cnt, wsum);
+}
+
+// chunking of the one-launch kernels: >= min_rc rows per chunk, about `blocks` workgroups
+int64_t stats1_chunks(int64_t R, int64_t C, int win, int64_t blocks, int64_t min_rc, int64_t* rc) {
+  const int64_t bx = cdiv(C, win);
+  const int64_t n = std::max<int64_t>(1, std::min<int64_t>(cdiv(R, min_rc), cdiv(blocks, bx)));
+  *rc = cdiv(R, n);
+  return cdiv(R, *rc);
+}
+int wmean_win(int64_t g) { return (int)std::max<int64_t>(128, g); }
+
 // ----------------------------------------------- a5: grid-search loss sum((a - b)^2)
 // [3P] llmcompressor _compute_loss over a parent's outputs: (fp16_out - q_out) in the output
 // dtype (bf16), squared in f32, summed (here in f64, fixed order: deterministic).
@@ -419,10 +593,16 @@ bool v8_ok(const void* w, int64_t C, int64_t ld, const float* s, bool cols) {
 
 extern "C" {
 
+static bool absmean_1l(int64_t channels) { return QZ_STATS_1L && cdiv(channels, 128) <= STATS_CNT; }
+
 size_t qz_awq_absmean_workspace_size(int64_t tokens, int64_t channels) {
   if (tokens <= 0 || channels <= 0) return 0;
   int64_t tc;
-  const int64_t nch = absmean_chunks(tokens, channels, &tc);
+  const int64_t nch = absmean_chunks(tokens, channels, &tc);  // the two-launch path's slab
+  if (absmean_1l(channels)) {  // (that path still serves unaligned inputs, after the counters)
+    const int64_t n1 = stats1_chunks(tokens, channels, 128, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &tc);
+    return (size_t)STATS_HEAD + (size_t)4 * (size_t)(std::max(n1, nch) * channels);
+  }
   return (size_t)4 * (size_t)(nch * channels);
 }
 
@@ -438,6 +618,15 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   float* part = (float*)workspace;
   const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16) &&
                   tokens < INT32_MAX && ld < INT32_MAX;
+  if (v8 && absmean_1l(channels)) {
+    int64_t rc1;
+    const int64_t n1 = stats1_chunks(tokens, channels, 128, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &rc1);
+    hipLaunchKernelGGL(k_absmean_1l<128>, dim3((unsigned)cdiv(channels, 128), (unsigned)n1), dim3(QZ_ABS1_WPB * 64),
+                       0, st, (const uint16_t*)x, tokens, channels, ld, rc1, n1,
+                       (float*)((char*)workspace + STATS_HEAD), (unsigned*)workspace, sum);
+    return launch_err();
+  }
+  if (absmean_1l(channels)) part = (float*)((char*)workspace + STATS_HEAD);  // same workspace layout
   if (v8) {
     dim3 grid((unsigned)cdiv(channels, 512), (unsigned)nch);
     hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(AWP * 64), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
@@ -529,9 +718,14 @@ int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part
   return launch_err();
 }
 
+static bool wmean_1l(int64_t cols, int64_t g) { return QZ_STATS_1L && cdiv(cols, wmean_win(g)) <= STATS_CNT; }
+
 size_t qz_awq_weight_mean_workspace_size(int64_t rows, int64_t cols, int32_t group_size) {
   if (rows <= 0 || cols <= 0 || group_size <= 0) return 0;
   int64_t rc;
+  if (wmean_1l(cols, group_size))
+    return (size_t)STATS_HEAD +
+           (size_t)8 * (size_t)(stats1_chunks(rows, cols, wmean_win(group_size), QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc) * cols);
   return (size_t)8 * (size_t)(wmean_chunks(rows, cols, &rc) * cols);
 }
 
@@ -547,12 +741,30 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
     if (!workspace || workspace_bytes < qz_awq_weight_mean_workspace_size(rows, cols, group_size))
       return QZ_ERR_WORKSPACE;
     if (!aligned(workspace, 8)) return QZ_ERR_ALIGN;
-    int64_t rc;
-    const int64_t nch = wmean_chunks(rows, cols, &rc);
-    dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nch);
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const uint16_t* wp = (const uint16_t*)w;
+    if (wmean_1l(cols, g)) {
+      int64_t rc1;
+      const int win = wmean_win(g);
+      const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc1);
+      dim3 grid1((unsigned)cdiv(cols, win), (unsigned)n1), blk1(QZ_WM1_WPB * 64);
+      double* p1 = (double*)((char*)workspace + STATS_HEAD);
+      unsigned* cnt = (unsigned*)workspace;
+      switch (logl) {
+        case 0: hipLaunchKernelGGL((k_wmean_1l<128, 0>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        case 1: hipLaunchKernelGGL((k_wmean_1l<128, 1>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        case 2: hipLaunchKernelGGL((k_wmean_1l<128, 2>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        case 3: hipLaunchKernelGGL((k_wmean_1l<128, 3>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        case 4: hipLaunchKernelGGL((k_wmean_1l<128, 4>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        case 5: hipLaunchKernelGGL((k_wmean_1l<256, 5>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+        default: hipLaunchKernelGGL((k_wmean_1l<512, 6>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
+      }
+      return launch_err();
+    }
+    int64_t rc;
+    const int64_t nch = wmean_chunks(rows, cols, &rc);
+    dim3 grid((unsigned)cdiv(cols, 512), (unsigned)nch);
     double* part = (double*)workspace;
     switch (logl) {
       case 0: hipLaunchKernelGGL(k_wmean_v8<0>, grid, dim3(WWP * 64), 0, st, wp, rows, cols, ld, rc, part); break;
@@ -572,6 +784,32 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
                        cols, ld, g, wsum);
   }
   return launch_err();
+}
+
+int qz_awq_stats_layout(int32_t which, int64_t rows, int64_t cols, int32_t group_size, int64_t* out) {
+  if (!out) return QZ_ERR_NULL;
+  if (rows <= 0 || cols <= 0 || (which != 0 && which != 1) || (which == 1 && group_size <= 0)) return QZ_ERR_SHAPE;
+  const bool one = which == 0 ? absmean_1l(cols) : (wmean_1l(cols, group_size) && group_size >= 8 &&
+                                                   group_size <= 512 && (group_size & (group_size - 1)) == 0);
+  int64_t rc = 0, nch = 0;
+  int win = 512, swp = which == 0 ? AWP : WWP, tf = FW;
+  if (one) {
+    win = which == 0 ? 128 : wmean_win(group_size);
+    swp = which == 0 ? QZ_ABS1_WPB : QZ_WM1_WPB;
+    nch = which == 0 ? stats1_chunks(rows, cols, win, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &rc)
+                     : stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc);
+    tf = swp * 64 / win;
+  } else {
+    nch = which == 0 ? absmean_chunks(rows, cols, &rc) : wmean_chunks(rows, cols, &rc);
+  }
+  out[0] = one;
+  out[1] = win;
+  out[2] = rc;
+  out[3] = nch;
+  out[4] = (int64_t)swp * 64 / (win / 8);  // row slots per workgroup
+  out[5] = tf;
+  out[6] = one ? STATS_HEAD : 0;
+  return QZ_OK;
 }
 
 int qz_awq_grid_scales(const float* x_mean, const float* w_mean, int64_t channels, float ratio, int32_t duo_scaling,

@@ -620,25 +620,46 @@ __device__ __forceinline__ f32x2 unpk(const uint32_t u) {
 // qparams -> quantize -> dequantize -> bf16(fl32(dq / s)); the same op sequence as
 // encode_store<KIND, FQ=true> (compressed-tensors' fake_quantize on the scaled weight, then the
 // f32 division by the column scales)
+#ifndef QZ_FQ_MAX3
+#define QZ_FQ_MAX3 1  // symmetric fake-quant: f32 |max| by v_max3 (1) or packed u16 maxima (0); A/B knob
+#endif
 template <int LOGL, int KIND, bool SYM>
 __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2* cs, const f32x2* rc, const bool cs_ok) {
   constexpr int L = 1 << LOGL;
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
-  uint32_t xw[4];
   f32x2 x[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    xw[k] = pk_bf16(unpk(wd[k]) * cs[k]);  // W * s in the weight dtype
-    x[k] = unpk(xw[k]);
-  }
   float mn, mx;
+#if QZ_FQ_MAX3
+  // W * s rounded to bf16 straight into f32 lanes (bfr2: one convert per element) and the
+  // group's |max| by three-input maxima with |.| source modifiers (4 VALU for 8 elements);
+  // the inputs are finite (D12), so the maximum is exact and order-free
+  if (SYM) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = bfr2(unpk(wd[k]) * cs[k]);
+    float m0, m1, m2, m3;
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m0) : "v"(x[0].x), "v"(x[0].y), "v"(x[1].x));
+    asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(m1) : "v"(x[1].y), "v"(x[2].x), "v"(x[2].y));
+    asm("v_max3_f32 %0, %1, %2, |%3|" : "=v"(m2) : "v"(m0), "v"(m1), "v"(x[3].x));
+    asm("v_max_f32 %0, %1, |%2|" : "=v"(m3) : "v"(m2), "v"(x[3].y));
+    mx = __uint_as_float(grp_max_u<L>(__float_as_uint(m3)));
+    mn = -mx;
+  } else
+#endif
   if (SYM) {  // |bf16| bit patterns, two per dword
+    uint32_t xw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xw[k] = pk_bf16(unpk(wd[k]) * cs[k]);  // W * s in the weight dtype
+      x[k] = unpk(xw[k]);
+    }
     const uint32_t m = pk_max_u16(pk_max_u16(xw[0] & 0x7fff7fffu, xw[1] & 0x7fff7fffu),
                                   pk_max_u16(xw[2] & 0x7fff7fffu, xw[3] & 0x7fff7fffu));
     const uint32_t am = grp_max_u<L>(max(m & 0xffffu, m >> 16) << 16);
     mx = __uint_as_float(am);
     mn = -mx;
   } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = bfr2(unpk(wd[k]) * cs[k]);  // W * s in the weight dtype
     uint32_t kmn = 0xffffffffu, kmx = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

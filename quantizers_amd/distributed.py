@@ -9,7 +9,10 @@ scripts/quant_GLM-4.7-Flash-FP8.py:22).  Quantize+pack has no cross-weight depen
 * each rank compresses its share with the fused HIP kernel -- no collective on the data path;
 * ``gather_state`` flattens each rank's compressed tensors into one byte buffer and runs ONE
   ``all_gather_into_tensor`` (padded to the largest shard; xGMI is point-to-point, so a single
-  large collective beats many small ones), then every rank unflattens the full state dict.
+  large collective beats many small ones) straight into the result buffer, whose per-rank
+  slices every rank unflattens as views -- or ``gather`` to one rank only (``dst``).
+* ``save_compressed`` does not gather at all: each rank writes its own shard files
+  (``compressor.save_compressed``).
 
 Works with backend "nccl" (RCCL, GPU tensors) and "gloo" (CPU tensors, used by the CPU tests).
 """
@@ -36,9 +39,9 @@ def plan_shards(items: Sequence[Item], world: int) -> List[List[str]]:
     return out
 
 
-def _flatten(tensors: Dict[str, torch.Tensor], device) -> Tuple[torch.Tensor, List[Tuple[str, str, Tuple[int, ...], int]]]:
-    """Pack ``tensors`` (sorted by name) into one uint8 buffer on ``device``, every tensor 16-B
-    aligned; returns the buffer and [(name, dtype, shape, byte offset)]."""
+def _layout(tensors: Dict[str, torch.Tensor]) -> Tuple[int, List[Tuple[str, str, Tuple[int, ...], int]]]:
+    """Byte layout of ``tensors`` (sorted by name) in one flat buffer, every tensor 16-B aligned:
+    (total bytes, [(name, dtype, shape, byte offset)])."""
     meta = []
     off = 0
     for k in sorted(tensors):
@@ -46,24 +49,45 @@ def _flatten(tensors: Dict[str, torch.Tensor], device) -> Tuple[torch.Tensor, Li
         nb = t.numel() * t.element_size()
         meta.append((k, str(t.dtype).replace("torch.", ""), tuple(t.shape), off))
         off += (nb + 15) // 16 * 16
-    flat = torch.zeros(off, dtype=torch.uint8, device=device)
-    for k, _, _, o in meta:
+    return off, meta
+
+
+def _flatten(tensors: Dict[str, torch.Tensor], device, meta=None, capacity: Optional[int] = None) -> torch.Tensor:
+    """Copy ``tensors`` into one uint8 buffer of ``capacity`` bytes (default: the layout's size)
+    on ``device`` at the offsets of ``meta`` (``_layout``); the padding is zeroed."""
+    size, lay = _layout(tensors) if meta is None else (None, meta)
+    if size is None:
+        last = lay[-1] if lay else None
+        size = 0 if last is None else last[3] + (_nbytes(last) + 15) // 16 * 16
+    cap = size if capacity is None else capacity
+    flat = torch.empty(cap, dtype=torch.uint8, device=device)
+    end = 0
+    for k, _, _, o in lay:
         t = tensors[k].contiguous()
         nb = t.numel() * t.element_size()
+        if o > end:
+            flat[end:o].zero_()
         if nb:
             flat[o:o + nb].copy_(t.reshape(-1).view(torch.uint8), non_blocking=True)
-    return flat, meta
+        end = o + nb
+    if cap > end:
+        flat[end:].zero_()
+    return flat
+
+
+def _nbytes(entry) -> int:
+    _, dt, shape, _ = entry
+    n = 1
+    for d in shape:
+        n *= d
+    return n * torch.empty((), dtype=getattr(torch, dt)).element_size()
 
 
 def _unflatten(flat: torch.Tensor, meta, copy: bool = True) -> Dict[str, torch.Tensor]:
     out = {}
-    for k, dt, shape, off in meta:
-        dtype = getattr(torch, dt)
-        n = 1
-        for d in shape:
-            n *= d
-        nb = n * torch.empty((), dtype=dtype).element_size()
-        t = flat[off:off + nb].view(dtype).reshape(shape)
+    for ent in meta:
+        k, dt, shape, off = ent
+        t = flat[off:off + _nbytes(ent)].view(getattr(torch, dt)).reshape(shape)
         out[k] = t.clone() if copy else t
     return out
 
@@ -76,11 +100,14 @@ def gather_state(local: Dict[str, torch.Tensor], device=None, dst: Optional[int]
     """Reassemble every rank's tensors: the union of all ranks' ``local`` dicts on every rank
     (``dst=None``) or on rank ``dst`` only (the other ranks return ``{}``).
 
-    Each rank's tensors are packed into one flat byte buffer; the buffers (padded to the largest
-    rank's size) travel in rounds of ``bucket_bytes`` per rank, one ``all_gather_into_tensor``
-    per round -- a few large RCCL collectives over the point-to-point xGMI links rather than one
-    per tensor, with a bounded staging footprint.  ``to_host``: the receivers' results land in
-    pinned host memory (the writer's input), otherwise on ``device``."""
+    Each rank's tensors are packed into one flat byte buffer (padded to the largest rank's size).
+    ``dst=None``: the buffers travel by ``all_gather_into_tensor`` -- ONE collective straight into
+    the result buffer when every rank's share fits ``bucket_bytes``, otherwise rounds of
+    ``bucket_bytes`` per rank (a bounded staging footprint); a few large RCCL collectives over the
+    point-to-point xGMI links rather than one per tensor.  ``dst=r``: the same rounds by
+    ``gather`` to rank ``r`` alone (no bytes delivered to ranks that drop them).  ``to_host``:
+    the receivers' results land in pinned host memory (the writer's input), otherwise on
+    ``device``."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     if world == 1:
         if not to_host:
@@ -97,24 +124,45 @@ def _gather_packed(local: Dict[str, torch.Tensor], device, dst: Optional[int], t
     nccl = dist.get_backend() == "nccl"
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
-    flat, meta = _flatten(local, device)
+    size, meta = _layout(local)
     metas: List = [None] * world
-    dist.all_gather_object(metas, (flat.numel(), meta))
+    dist.all_gather_object(metas, (size, meta))
     maxn = max(m[0] for m in metas)
     receiver = dst is None or rank == dst
+    out: Dict[str, torch.Tensor] = {}
+    if maxn == 0:
+        return out if receiver else {}
+    if maxn <= bucket_bytes and not to_host:
+        # one round, received in place: rank r's tensors are views of recv[r * maxn:]
+        send = _flatten(local, device, meta, capacity=maxn)
+        if dst is None:
+            recv = torch.empty(world * maxn, dtype=torch.uint8, device=device)
+            dist.all_gather_into_tensor(recv, send)
+        else:
+            recv = torch.empty(world * maxn, dtype=torch.uint8, device=device) if receiver else None
+            dist.gather(send, [recv[r * maxn:(r + 1) * maxn] for r in range(world)] if receiver else None, dst=dst)
+        if not receiver:
+            return {}
+        for r in range(world):
+            out.update(_unflatten(recv[r * maxn:(r + 1) * maxn], metas[r][1], copy=False))
+        return out
+    flat = _flatten(local, device, meta)
     host_dev = torch.device("cpu") if to_host else torch.device(device)
     pin = to_host and flat.is_cuda
     dest = [torch.empty(metas[r][0], dtype=torch.uint8, device=host_dev, pin_memory=pin) for r in range(world)] \
         if receiver else None
-    step = max(16, min(bucket_bytes, maxn) // 16 * 16) if maxn else 16
+    step = max(16, min(bucket_bytes, maxn) // 16 * 16)
     send = torch.zeros(step, dtype=torch.uint8, device=device)
-    recv = torch.empty(world * step, dtype=torch.uint8, device=device)
+    recv = torch.empty(world * step, dtype=torch.uint8, device=device) if receiver else None
     for off in range(0, maxn, step):
         n = min(step, maxn - off)
         valid = max(0, min(n, flat.numel() - off))
         if valid:
             send[:valid].copy_(flat[off:off + valid])
-        dist.all_gather_into_tensor(recv[: world * n], send[:n])
+        if dst is None:
+            dist.all_gather_into_tensor(recv[: world * n], send[:n])
+        else:
+            dist.gather(send[:n], [recv[r * n:(r + 1) * n] for r in range(world)] if receiver else None, dst=dst)
         if receiver:
             for r in range(world):
                 take = max(0, min(n, metas[r][0] - off))
@@ -124,7 +172,6 @@ def _gather_packed(local: Dict[str, torch.Tensor], device, dst: Optional[int], t
         return {}
     if pin:
         torch.cuda.current_stream(device).synchronize()
-    out: Dict[str, torch.Tensor] = {}
     for r in range(world):
         out.update(_unflatten(dest[r], metas[r][1], copy=False))
     return out

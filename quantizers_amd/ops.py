@@ -47,6 +47,7 @@ def _check_dev(t: torch.Tensor, name: str):
 
 
 _ws_cache: Dict[Tuple[int, int], torch.Tensor] = {}
+_stats_ws_cache: Dict[Tuple[int, int], torch.Tensor] = {}
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:
@@ -58,6 +59,29 @@ def workspace(nbytes: int, device) -> torch.Tensor:
         buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
         _ws_cache[key] = buf
     return buf
+
+
+def stats_workspace(nbytes: int, device) -> torch.Tensor:
+    """Per-(device, stream) grow-only scratch of the AWQ statistics calls, zeroed when allocated:
+    its head holds the one-launch reduction's arrival counters, which every call leaves zero
+    (quantizers_amd.h, statistics workspace contract) -- so it is never shared with other calls."""
+    dev = torch.device(device)
+    key = (dev.index or 0, torch.cuda.current_stream(dev).cuda_stream)
+    buf = _stats_ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+        _stats_ws_cache[key] = buf
+    return buf
+
+
+def awq_stats_layout(which: str, rows: int, cols: int, group_size: int = 0) -> Dict[str, int]:
+    """The fixed summation plan of awq_absmean_accum (``which="absmean"``, rows = tokens) or
+    awq_weight_mean_accum (``"wmean"``) for a [rows, cols] input (qz_awq_stats_layout)."""
+    out = (ctypes.c_int64 * 7)()
+    rc = _lib.load().qz_awq_stats_layout(0 if which == "absmean" else 1, rows, cols, int(group_size), out)
+    _lib.check(rc, "qz_awq_stats_layout")
+    return dict(zip(("one_launch", "window", "rows_per_chunk", "chunks", "slots", "final_groups", "head_bytes"),
+                    list(out)))
 
 
 def _geom(w: torch.Tensor):
@@ -508,7 +532,7 @@ def awq_absmean_accum(x: torch.Tensor, sums: torch.Tensor) -> int:
         x2 = x2.contiguous()
     t, c = x2.shape
     lib = _lib.load()
-    ws = workspace(lib.qz_awq_absmean_workspace_size(t, c) + 256, x.device)
+    ws = stats_workspace(lib.qz_awq_absmean_workspace_size(t, c) + 256, x.device)
     rc = lib.qz_awq_absmean_accum(_ptr(x2), t, c, x2.stride(0), _ptr(sums), _ptr(ws), ws.numel(), _stream())
     _lib.check(rc, "qz_awq_absmean_accum")
     return t
@@ -516,14 +540,14 @@ def awq_absmean_accum(x: torch.Tensor, sums: torch.Tensor) -> int:
 
 def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) -> int:
     """wsum[c] += sum_r |W[r,c]| / (group absmax + 1e-6) (fp64, deterministic: fixed-order
-    two-stage reduction).  Returns rows added."""
+    reduction, ``awq_stats_layout``).  Returns rows added."""
     _check_dev(w, "weight")
     w2 = w.reshape(-1, w.shape[-1])
     if w2.stride(-1) != 1:
         w2 = w2.contiguous()
     r, c = w2.shape
     lib = _lib.load()
-    ws = workspace(lib.qz_awq_weight_mean_workspace_size(r, c, int(group_size)) + 256, w.device)
+    ws = stats_workspace(lib.qz_awq_weight_mean_workspace_size(r, c, int(group_size)) + 256, w.device)
     rc = lib.qz_awq_weight_mean_accum(_ptr(w2), r, c, w2.stride(0), int(group_size), _ptr(wsum), _ptr(ws), ws.numel(),
                                       _stream())
     _lib.check(rc, "qz_awq_weight_mean_accum")

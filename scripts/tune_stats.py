@@ -37,8 +37,8 @@ def main():
         lib = bind(path)
         na = lib.qz_awq_absmean_workspace_size(T, C)
         nw = lib.qz_awq_weight_mean_workspace_size(R, C, G)
-        b = {"name": path.split("/")[-1], "lib": lib, "wa": torch.empty(na, dtype=torch.uint8, device=dev),
-             "ww": torch.empty(nw, dtype=torch.uint8, device=dev),
+        b = {"name": path.split("/")[-1], "lib": lib, "wa": torch.zeros(na, dtype=torch.uint8, device=dev),
+             "ww": torch.zeros(nw, dtype=torch.uint8, device=dev),
              "sa": torch.zeros(C, dtype=torch.float32, device=dev),
              "sw": torch.zeros(C, dtype=torch.float64, device=dev), "ta": [], "tw": []}
 

@@ -143,7 +143,7 @@ def _tiny_model():
     return m
 
 
-def _save_worker(rank, world, port, out_dir, q):
+def _save_worker(rank, world, port, out_dir, shard_bytes, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -151,13 +151,23 @@ def _save_worker(rank, world, port, out_dir, q):
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
         from quantizers_amd import compressor
         compressor.CompressionPlan = _OraclePlan
-        compressor.save_compressed(_tiny_model(), out_dir, device="cpu")
-        q.put((rank, sorted(os.listdir(out_dir))))
+        written = []
+        real = compressor._write_shard_file
+
+        def spy(shard, path, ready):
+            written.append(os.path.basename(path))
+            real(shard, path, ready)
+        compressor._write_shard_file = spy
+        compressor.save_compressed(_tiny_model(), out_dir, max_shard_bytes=shard_bytes, device="cpu")
+        q.put((rank, sorted(os.listdir(out_dir)), sorted(written)))
     finally:
         dist.destroy_process_group()
 
 
-def test_save_compressed_gloo_world2_matches_one_process(tmp_path):
+@pytest.mark.parametrize("shard_bytes", [5 << 30, 6000])
+def test_save_compressed_gloo_world2_matches_one_process(tmp_path, shard_bytes):
+    """Each rank writes its own shards of the plan (no gather); the files are byte-identical to
+    one process, and with several shards both ranks write."""
     import filecmp
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
@@ -166,21 +176,31 @@ def test_save_compressed_gloo_world2_matches_one_process(tmp_path):
     q = ctx.Queue()
     port = _free_port()
     multi = str(tmp_path / "multi")
-    procs = [ctx.Process(target=_save_worker, args=(r, 2, port, multi, q)) for r in range(2)]
+    procs = [ctx.Process(target=_save_worker, args=(r, 2, port, multi, shard_bytes, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0][1] == res[1][1] and "model.safetensors" in res[0][1]
+    assert res[0][1] == res[1][1]
     saved = compressor.CompressionPlan
     compressor.CompressionPlan = _OraclePlan
     try:
-        one = compressor.save_compressed(_tiny_model(), str(tmp_path / "one"), device="cpu")
+        one = compressor.save_compressed(_tiny_model(), str(tmp_path / "one"), max_shard_bytes=shard_bytes,
+                                         device="cpu")
     finally:
         compressor.CompressionPlan = saved
-    for fn in ("model.safetensors", "config.json"):
+    files = sorted(os.listdir(one))
+    assert files == res[0][1]
+    shards = [f for f in files if f.endswith(".safetensors")]
+    assert sorted(res[0][2] + res[1][2]) == shards and not set(res[0][2]) & set(res[1][2])
+    if shard_bytes < 1 << 20:
+        assert len(shards) > 2 and res[0][2] and res[1][2]  # both ranks wrote
+        assert "model.safetensors.index.json" in files
+    else:
+        assert shards == ["model.safetensors"]
+    for fn in files:
         assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
 
 
@@ -190,11 +210,18 @@ def _gather_worker(rank, world, port, q):
     try:
         local = {f"r{rank}.t{i}": torch.arange(i * 7 + rank * 3 + 1, dtype=torch.int16) for i in range(5)}
         local[f"r{rank}.e"] = torch.empty(0, dtype=torch.float32)
-        # tiny buckets: several all-gather rounds, ragged per-rank sizes
-        out = gather_state(local, dst=1, to_host=True, bucket_bytes=64)
-        q.put((rank, {k: v.tolist() for k, v in out.items()}))
+        res = []
+        # tiny buckets: several rounds, ragged per-rank sizes; big buckets: one collective
+        # received in place; gather to one rank (dst) and all-gather to every rank (dst=None)
+        for dst, to_host, bucket in MODES:
+            out = gather_state(local, dst=dst, to_host=to_host, bucket_bytes=bucket)
+            res.append({k: v.tolist() for k, v in out.items()})
+        q.put((rank, res))
     finally:
         dist.destroy_process_group()
+
+
+MODES = [(1, True, 64), (None, False, 64), (None, False, 1 << 20), (2, False, 1 << 20), (0, False, 64)]
 
 
 def test_gather_state_buckets_and_dst():
@@ -208,7 +235,8 @@ def test_gather_state_buckets_and_dst():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert res[0] == {} and res[2] == {}
     want = {f"r{r}.t{i}": list(range(i * 7 + r * 3 + 1)) for r in range(3) for i in range(5)}
     want.update({f"r{r}.e": [] for r in range(3)})
-    assert res[1] == want
+    for m, (dst, _, _) in enumerate(MODES):
+        for r in range(3):
+            assert res[r][m] == (want if dst is None or dst == r else {}), (MODES[m], r)

@@ -145,6 +145,7 @@ def test_awq_stat_kernels_guard_band(cuda):
     lib = _lib.load()
     wsn = lib.qz_awq_absmean_workspace_size(T, Cc)
     wsp = ar.take((wsn,), torch.uint8)
+    wsp.zero_()  # statistics workspace contract: arrival counters zero before the first call
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
     assert lib.qz_awq_absmean_accum(P(x), T, Cc, Cc, P(sums), P(wsp), wsp.numel(), st) == 0
@@ -152,7 +153,10 @@ def test_awq_stat_kernels_guard_band(cuda):
     wsum.zero_()
     wmn = lib.qz_awq_weight_mean_workspace_size(T, Cc, 128)
     wmw = ar.take((max(wmn, 16),), torch.uint8)
+    wmw.zero_()
     assert lib.qz_awq_weight_mean_accum(P(x), T, Cc, Cc, 128, P(wsum), P(wmw), wmw.numel(), st) == 0
     ok, where = ar.intact()
     assert ok, where
     assert torch.allclose(sums.double(), x.float().abs().sum(0).double(), rtol=1e-5)
+    head = 32768  # QZ_STATS_HEAD_BYTES: every call leaves the arrival counters zero
+    assert not wsp[:head].any() and not wmw[:head].any()

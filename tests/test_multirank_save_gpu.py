@@ -1,7 +1,8 @@
 """Multi-rank product path on one card: ``oneshot`` (AWQ) + ``save_compressed`` under
-torch.distributed (2 ranks, gloo control plane sharing cuda:0) -- compression sharded over the
-ranks by ``plan_shards``, reassembled by ``gather_state``, written by rank 0 -- produces a
-checkpoint byte-identical to the one-process run."""
+torch.distributed (2 ranks, gloo control plane sharing cuda:0) -- each rank compressing and
+writing its own shards of the save plan (``compressor.save_plan``), rank 0 adding the index and
+config -- produces a checkpoint byte-identical to the one-process run, with one shard or with
+several (both ranks writing)."""
 import filecmp
 import os
 import socket
@@ -19,6 +20,9 @@ def _model_and_data():
     return _qwen3(layers=2), _calib()
 
 
+SHARD = 200 << 10  # the 2-layer model (about 1.3 MB of tensors) in several shards
+
+
 def _rank(rank, world, port, out_dir):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -31,6 +35,7 @@ def _rank(rank, world, port, out_dir):
         m = m.to("cuda:0")
         oneshot(m, RECIPE, dataset=data, max_seq_length=64)
         save_compressed(m, out_dir)
+        save_compressed(m, out_dir + "_sharded", max_shard_bytes=SHARD)
     finally:
         dist.destroy_process_group()
 
@@ -55,3 +60,9 @@ def test_save_compressed_two_ranks_byte_identical(cuda, tmp_path):
     one = save_compressed(m, str(tmp_path / "one_process"))
     for fn in ("model.safetensors", "config.json", "recipe.yaml"):
         assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
+    one = save_compressed(m, str(tmp_path / "one_process_sharded"), max_shard_bytes=SHARD)
+    files = sorted(os.listdir(one))
+    assert files == sorted(os.listdir(multi + "_sharded")) and "model.safetensors.index.json" in files
+    assert len([f for f in files if f.endswith(".safetensors")]) >= 2
+    for fn in files:
+        assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi + "_sharded", fn), shallow=False), fn

@@ -286,58 +286,83 @@ def test_absmean_ragged_windows(cuda, tokens, ch):
     assert torch.equal(sums[ch:].cpu(), torch.full((16,), 7.0))
 
 
-@pytest.mark.parametrize("rows,cols,g", [(1, 32, 32), (9, 96, 32), (45, 640, 128), (1001, 1088, 64)])
+@pytest.mark.parametrize("rows,cols,g", [(1, 32, 32), (9, 96, 32), (45, 640, 128), (1001, 1088, 64),
+                                         (700, 1024, 256), (300, 2048, 512), (5000, 136, 8)])
 def test_weight_mean_ragged_windows(cuda, rows, cols, g):
-    """w_mean with a partly empty last column window and row counts that are not multiples of
-    the waves per workgroup: the fixed-order tree, bit for bit."""
+    """w_mean with a partly empty last column window, row counts that are not multiples of the
+    row slots per workgroup, and every window width (128 / 256 / 512 columns): the fixed-order
+    tree, bit for bit."""
     w = _w(rows, cols, seed=rows)
     wsum = torch.zeros(cols, dtype=torch.float64, device=cuda)
     assert ops.awq_weight_mean_accum(w.to(cuda), g, wsum) == rows
     assert torch.equal(wsum.cpu(), _wmean_tree(w, g))
 
 
-def _wmean_tree(w: torch.Tensor, g: int) -> torch.Tensor:
-    """Fixed-order restatement of qz_awq_weight_mean_accum's reduction tree (one call into a
-    zero wsum; the build's defaults QZ_WMEAN_WPB = 8 waves, QZ_WMEAN_BLOCKS = 256, 16 rows minimum
-    per chunk): terms bf16(|w| / bf16(group absmax + 1e-6)) (the oracle's elementwise values),
-    summed in f64 exactly as the two kernels do -- per row chunk, wave j sums rows j, j+8, ... in
-    order, chunk = (((s0 + s1) + s2) + ...) + s7; then wave v of stage 2 sums chunks v, v+16, ...
-    and the 16 wave sums are added in order."""
+def _stats_tree(v, lay, dtype=None) -> "np.ndarray":
+    """Fixed-order restatement of the AWQ statistics reduction (ops.awq_stats_layout, f64 terms
+    ``v`` [R, C]).  One-launch plan: per row chunk, slot s sums rows s, s + S, ... in order, the
+    chunk partial is ((slot 0 + slot 1) + ...); the window's last workgroup then sums, for each of
+    the TF thread groups f, chunks f, f + TF, ... in order and adds the TF sums in order.  The
+    two-launch plan (wide channel counts) is the same with S = waves per workgroup and TF = 16."""
     import numpy as np
-    wpb, blocks = 8, 256
-    R, C = w.shape
-    v = w.reshape(-1, g).abs()
-    v = (v / (v.amax(dim=1, keepdim=True) + 1e-6)).reshape(R, C).double().numpy()
-    bx = -(-C // 512)
-    nrc = max(1, min(-(-R // 16), -(-blocks // bx)))
-    rc = -(-R // nrc)
-    nch = -(-R // rc)
-    part = np.zeros((nch, C))
+    R, C = v.shape
+    dt = v.dtype if dtype is None else dtype
+    rc, nch, S, TF = lay["rows_per_chunk"], lay["chunks"], lay["slots"], lay["final_groups"]
+    part = np.zeros((nch, C), dtype=dt)
     for k in range(nch):
         r0, r1 = k * rc, min(R, (k + 1) * rc)
         t = None
-        for j in range(wpb):
-            acc = np.zeros(C)
-            for r in range(r0 + j, r1, wpb):
+        for j in range(S):
+            acc = np.zeros(C, dtype=dt)
+            for r in range(r0 + j, r1, S):
                 acc = acc + v[r]
             t = acc if t is None else t + acc
         part[k] = t
     red = []
-    for wv in range(16):
-        acc = np.zeros(C)
-        for k in range(wv, nch, 16):
+    for f in range(TF):
+        acc = np.zeros(C, dtype=dt)
+        for k in range(f, nch, TF):
             acc = acc + part[k]
         red.append(acc)
     t = red[0]
-    for wv in range(1, 16):
-        t = t + red[wv]
-    return torch.from_numpy(np.zeros(C) + t)
+    for f in range(1, TF):
+        t = t + red[f]
+    return np.zeros(C, dtype=dt) + t
+
+
+@pytest.mark.parametrize("tokens,ch", [(2048, 2560), (16384, 4096), (333, 1032), (7, 264)])
+def test_absmean_fixed_order_bit_exact(cuda, tokens, ch):
+    """absmean's f32 sums equal the restated fixed-order tree bit for bit (one launch: the
+    last-arriving workgroup of each window adds the chunk partials), and the statistics
+    workspace's arrival counters are zero again after the call."""
+    import numpy as np
+    g = torch.Generator().manual_seed(tokens + ch)
+    x = torch.randn(tokens, ch, generator=g).to(torch.bfloat16)
+    sums = torch.zeros(ch, dtype=torch.float32, device=cuda)
+    ops.awq_absmean_accum(x.to(cuda), sums)
+    lay = ops.awq_stats_layout("absmean", tokens, ch)
+    want = _stats_tree(x.float().abs().numpy(), lay, np.float32)
+    assert torch.equal(sums.cpu(), torch.from_numpy(want))
+    torch.cuda.synchronize()
+    for buf in ops._stats_ws_cache.values():
+        assert not buf[:lay["head_bytes"]].any()
+
+
+def _wmean_tree(w: torch.Tensor, g: int) -> torch.Tensor:
+    """qz_awq_weight_mean_accum's sum for one call into a zero wsum: terms
+    bf16(|w| / bf16(group absmax + 1e-6)) (the oracle's elementwise values) summed in f64 in the
+    kernel's fixed order (``_stats_tree``)."""
+    R, C = w.shape
+    v = w.reshape(-1, g).abs()
+    v = (v / (v.amax(dim=1, keepdim=True) + 1e-6)).reshape(R, C).double().numpy()
+    return torch.from_numpy(_stats_tree(v, ops.awq_stats_layout("wmean", R, C, g)))
 
 
 @pytest.mark.parametrize("shape,g", [((320, 512), 32), ((2000, 1536), 128), ((37, 4096), 64)])
 def test_weight_mean_deterministic_fixed_order(cuda, shape, g):
-    """w_mean is a fixed-order two-stage reduction: bit-identical to the restated tree, and
-    identical across repeated calls while other work runs concurrently on another stream."""
+    """w_mean is a fixed-order one-launch reduction: bit-identical to the restated tree, and
+    identical across repeated calls while other work runs concurrently on another stream (the
+    last-arriving workgroup differs from call to call; the order does not)."""
     w = _w(*shape, seed=11)
     wc = w.to(cuda)
     want = _wmean_tree(w, g)
