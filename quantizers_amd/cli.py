@@ -10,8 +10,10 @@ checkpoint (do_oneshot.py:198).  Offline additions (no Hub access in this enviro
 ``model.name``'s architecture from a local config with random weights), --tokenizer (a local
 tokenizer directory when the model has none), --calib-file (tokenized calibration set: .pt
 tensor [N, S] or .jsonl rows with ``input_ids``) and --calib-random N,S (synthetic token ids).
-Under torchrun every rank runs the calibration (AWQ grid ratios / expert searches split over the
-ranks) and the compression is sharded; rank 0 alone writes the output directory.
+Under torchrun rank 0 alone loads the model (the others hold a meta skeleton and receive each
+decoder layer by broadcast, ``residency``), every rank runs the calibration (AWQ grid ratios /
+expert searches split over the ranks), and each rank compresses and writes its own shards of the
+checkpoint; rank 0 adds the index and config.
 """
 from __future__ import annotations
 
@@ -101,7 +103,15 @@ def load_tokenizer(args, run):
 
 
 def load_model(args, run):
+    """The model in bf16 on the host (do_oneshot.py:86-94).  Under torchrun only rank 0 loads the
+    weights; the other ranks build a meta-device skeleton of the same architecture and receive
+    each decoder layer by broadcast as the AWQ pass reaches it (``residency``): one host copy
+    of the model for the whole job (QZ_RANK_COPIES=1 restores one copy per rank)."""
     from transformers import AutoConfig, AutoModelForCausalLM
+    if _rank() != 0 and os.environ.get("QZ_RANK_COPIES", "0") != "1":
+        cfg = AutoConfig.from_pretrained(args.random_init or args.model_path or run.model.name, trust_remote_code=True)
+        with torch.device("meta"):
+            return AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
     if args.random_init:
         # offline stand-in for from_pretrained: random weights of the config's architecture, host
         # resident like a loaded checkpoint.  Initialised on the GPU (seconds; the CPU init of a
@@ -176,7 +186,7 @@ def main(argv=None):
         os.makedirs("outputs", exist_ok=True)
     logging.info("Saving quantized model to: %s", output_dir)
     t0 = time.time()
-    save_compressed(model, output_dir)  # sharded over ranks under torchrun; rank 0 writes
+    save_compressed(model, output_dir)  # under torchrun each rank writes its own shards
     if tokenizer is not None and _rank() == 0:
         tokenizer.save_pretrained(output_dir)
     logging.info("Saved quantized model in %.2f seconds", time.time() - t0)

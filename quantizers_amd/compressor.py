@@ -423,7 +423,17 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
     units, raw = compression_units(model)
     world, rank = _dist_info()
     mine = units
-    if world > 1:
+    res = getattr(model, "quantization_residency", None)
+    owned_raw: Dict[str, torch.Tensor] = {}
+    if world > 1 and res is not None:
+        # owner-keeps residency (oneshot over a meta skeleton): compress what this rank holds --
+        # a unit kept by two ranks (it straddles their shards) is taken by the lower one
+        sp = save_plan(units, raw, world, res.max_shard_bytes)
+        taken = set().union(*[set(sp.units_of[r]) for r in range(rank)]) if rank else set()
+        mine = [units[i] for i in sp.units_of[rank] if i not in taken]
+        if dst is None or dst != 0:  # receivers other than rank 0 get each unchanged tensor from its owner
+            owned_raw = {k: raw[k] for k in sp.raw_of[rank] if not raw[k].is_meta}
+    elif world > 1:
         from .distributed import plan_shards
         plan = plan_shards([(str(i), u.nbytes) for i, u in enumerate(units)], world)
         keep = {int(k) for k in plan[rank]}
@@ -439,9 +449,16 @@ def compressed_state_dict(model: nn.Module, device=None, to_host: bool = True,
     receiver = world == 1 or dst is None or rank == dst
     if world > 1:
         from .distributed import gather_state
+        local.update({f"\0raw.{k}": v for k, v in owned_raw.items()})
         local = gather_state(local, dst=dst, to_host=to_host)
+        # unchanged tensors a skeleton rank holds only as meta come from their owners
+        for k in [k for k in local if k.startswith("\0raw.")]:
+            v = local.pop(k)
+            if raw.get(k[5:]) is not None and raw[k[5:]].is_meta:
+                raw[k[5:]] = v
     if not receiver:
         return {}
+    raw = {k: v for k, v in raw.items() if not v.is_meta}
     out = dict(local)
     if to_host:
         host_raw, rc = _raw_to_host(raw, device)
@@ -574,6 +591,11 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
         # so a later model.config.save_pretrained(output_dir) keeps the compressed-tensors config
         model.config.quantization_config = qcfg
     t0 = time.perf_counter()
+    res = getattr(model, "quantization_residency", None)
+    if res is not None and (res.max_shard_bytes != max_shard_bytes or res.world != world):
+        raise ValueError(f"this model's ranks keep the tensors of a {res.world}-rank save plan with "
+                         f"max_shard_bytes={res.max_shard_bytes} (oneshot(max_shard_bytes=...)); "
+                         f"save_compressed was called with {world} rank(s) and {max_shard_bytes}")
     units, raw = compression_units(model)
     plan = save_plan(units, raw, world, max_shard_bytes)
     mine = [units[i] for i in plan.units_of[rank]]

@@ -113,7 +113,7 @@ def _layer_out(o):
 
 @torch.no_grad()
 def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report,
-                    calibrate_all_experts: bool = True, stateful_observers: bool = False):
+                    calibrate_all_experts: bool = True, stateful_observers: bool = False, residency=None):
     layers = decoder_layers(model)
     lname = next(n for n, m in model.named_modules() if m is layers)
     weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
@@ -122,14 +122,20 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
     mtype = model_type(model)
     stager = None
     batched: Optional[bool] = None  # per-sample layer calls run as one batched call (checked on layer 0)
+    def onload(layer):
+        nonlocal stager
+        if stager is None:
+            from .staging import H2DStager
+            stager = H2DStager(device)
+        return _onload(layer, stager)
+
     for i, layer in enumerate(layers):
         home = next(layer.parameters()).device
         host = None
-        if home != device:  # layer-by-layer onload: pinned staging, the host tensors kept for the offload
-            if stager is None:
-                from .staging import H2DStager
-                stager = H2DStager(device)
-            host = _onload(layer, stager)
+        if residency is not None:  # rank 0 onloads if needed, then one broadcast to every rank
+            host = residency.fetch(layer, onload)
+        elif home != device:  # layer-by-layer onload: pinned staging, the host tensors kept for the offload
+            host = onload(layer)
         t0 = time.time()
         if batched is None:
             batched = BATCH_LAYER_CALLS and _batched_forward_ok(layer, inputs)
@@ -147,6 +153,8 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
                 out = _layer_out(layer(*args, **kwargs))
                 nxt.append(((out,) + tuple(args[1:]), kwargs))
         inputs = nxt
+        if residency is not None:  # the other ranks keep only the tensors of their own shards
+            residency.release(layer)
         if host is not None:
             _offload(layer, host)
         log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), time.time() - t0)
@@ -156,7 +164,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             max_seq_length: Optional[int] = 2048, num_calibration_samples: Optional[int] = 512,
             moe_calibrate_all_experts: bool = True, device: Union[str, torch.device, None] = None,
             output_dir: Optional[str] = None, stateful_observers: bool = False,
-            device_resident: Optional[bool] = None, **kwargs) -> nn.Module:
+            device_resident: Optional[bool] = None, max_shard_bytes: Optional[int] = None,
+            **kwargs) -> nn.Module:
     """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
     scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
     dataset is already tokenized).  ``moe_calibrate_all_experts``: AWQ statistics and loss
@@ -168,7 +177,12 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     ``device_resident``: a host-resident model is moved to ``device`` for the AWQ pass and left
     there (True), or only its decoder layers are onloaded one at a time and returned to the host
     (False, the reference's placement); default: resident when its parameters take at most
-    half of the device's free memory."""
+    half of the device's free memory.
+
+    Under torch.distributed with a meta-device skeleton on every rank but 0
+    (``residency.Residency``, BASELINE configs[4]): rank 0's layers are broadcast as the pass
+    reaches them and each rank keeps only the tensors of the checkpoint shards it will write
+    (``max_shard_bytes``: the shard size ``save_compressed`` will be called with)."""
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -177,12 +191,19 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     if not schemes:
         raise ValueError("recipe targets no module of this model")
     report: Dict[str, Any] = {}
+    model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}  # the residency plan reads it
+    from . import residency as residency_mod
+    res = None
+    if residency_mod.skeleton_mode(model):
+        from .compressor import SHARD_BYTES
+        res = residency_mod.Residency(model, device, max_shard_bytes or SHARD_BYTES)
+        model.quantization_residency = res
     awqs = [m for m in modifiers if isinstance(m, AWQModifier)]
     if awqs:
         batches = _batches(dataset, num_calibration_samples, max_seq_length, device)
         if not batches:
             raise ValueError("AWQModifier needs a calibration dataset")
-        if next(model.parameters()).device.type == "cpu":
+        if next(model.parameters()).device.type == "cpu" and (res is None or res.rank == 0):
             if device_resident if device_resident is not None else _fits_on_device(model, device):
                 # 288 GB of HBM: a model that fits moves to the device once and stays there (no
                 # per-layer onload / offload over PCIe; save_compressed then needs no staging)
@@ -194,11 +215,23 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                 # embeddings / rotary / final norm run on the device; layers are onloaded one
                 # by one (the reference's sequential-pipeline placement)
                 _to_device_except(model, decoder_layers(model), device)
+        if res is not None:
+            res.materialise_outside(model, decoder_layers(model))
         # MoE experts in the reference's (transformers 4.57) eager arithmetic, at grouped speed (D15)
         with eager_experts(model):
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
-                                stateful_observers)
+                                stateful_observers, residency=res)
+    elif res is not None:  # RTN: no calibration pass, but each rank still needs its shards' tensors
+        stager = []
+
+        def onload(layer):
+            if not stager:
+                from .staging import H2DStager
+                stager.append(H2DStager(device))
+            return _onload(layer, stager[0])
+        res.materialise_outside(model, decoder_layers(model))
+        res.distribute(model, decoder_layers(model), onload, _offload)
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
     model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml

@@ -66,3 +66,46 @@ def test_save_compressed_two_ranks_byte_identical(cuda, tmp_path):
     assert len([f for f in files if f.endswith(".safetensors")]) >= 2
     for fn in files:
         assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi + "_sharded", fn), shallow=False), fn
+
+
+def _rank_skeleton(rank, world, port, out_dir):
+    """Rank 0 holds the model on the host (layer-by-layer onload), rank 1 a meta skeleton:
+    every decoder layer reaches rank 1 by broadcast, rank 1 keeps only its shards' tensors."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from transformers import AutoModelForCausalLM
+        from quantizers_amd.compressor import save_compressed
+        from quantizers_amd.oneshot import oneshot
+        m, data = _model_and_data()
+        if rank != 0:
+            with torch.device("meta"):
+                m = AutoModelForCausalLM.from_config(m.config, dtype=torch.bfloat16)
+        oneshot(m, RECIPE, dataset=data, max_seq_length=64, device="cuda:0", device_resident=False,
+                max_shard_bytes=SHARD)
+        if rank != 0:
+            n_meta = sum(p.is_meta for p in m.parameters())
+            assert 0 < n_meta < len(list(m.parameters())), n_meta
+        save_compressed(m, out_dir, max_shard_bytes=SHARD)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_skeleton_rank_save_byte_identical(cuda, tmp_path):
+    """One host copy of the model for two ranks (residency.Residency): the checkpoint equals the
+    one-process run's, byte for byte."""
+    import torch.multiprocessing as mp
+    from quantizers_amd.compressor import save_compressed
+    from quantizers_amd.oneshot import oneshot
+    multi = str(tmp_path / "skeleton")
+    mp.spawn(_rank_skeleton, args=(2, _port(), multi), nprocs=2, join=True)
+    m, data = _model_and_data()
+    m = m.to(cuda)
+    oneshot(m, RECIPE, dataset=data, max_seq_length=64)
+    one = save_compressed(m, str(tmp_path / "one"), max_shard_bytes=SHARD)
+    files = sorted(os.listdir(one))
+    assert files == sorted(os.listdir(multi)) and len([f for f in files if f.endswith(".safetensors")]) >= 2
+    for fn in files:
+        assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
