@@ -214,7 +214,16 @@ __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int
 }
 
 // combine the slots of this workgroup into part[chunk][c], then the window's last arriver sums
-// the chunks into sum[c] (see the order above) and resets the window's counter
+// the chunks into sum[c] (see the order above) and resets the window's counter.
+// Memory ordering without a device-scope fence (an agent-scope release writes the whole L2 back
+// and serialised the first version: 0.25-0.35 us per workgroup, profiles/r03b_tune_stats_fence.log):
+// the partials are written with agent-coherent (sc1) stores, every thread waits for its own
+// stores to complete (s_waitcnt 0) before the workgroup barrier, thread 0 then arrives with a
+// relaxed agent-scope atomic, and the last arriver reads the partials with agent-coherent loads.
+template <typename T>
+__device__ __forceinline__ void st_coherent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <int WIN, int SWP, typename T>
 __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int lane, int wv, int64_t C, int64_t nch,
                                              T* part, unsigned* cnt, T* sum) {
@@ -231,23 +240,22 @@ __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int la
       T t = red[0][j];
 #pragma unroll
       for (int k = 1; k < S; ++k) t += red[k][j];
-      part[(int64_t)blockIdx.y * C + c] = t;
+      st_coherent(part + (int64_t)blockIdx.y * C + c, t);
     }
   }
   __shared__ int last;
-  __threadfence();  // release this workgroup's partials at device scope before it arrives
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's partial stores have completed
   __syncthreads();
   if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
+    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
   __syncthreads();
   if (!last) return;
-  __threadfence();
   const int j = threadIdx.x % WIN, f = threadIdx.x / WIN;
   const int64_t c = cb + j;
   T t = 0;
   if (c < C) {
 #pragma unroll 4
-    for (int64_t k = f; k < nch; k += TF)  // coherent device-scope loads: partials of every XCD
+    for (int64_t k = f; k < nch; k += TF)  // coherent loads: partials written on every XCD
       t += __hip_atomic_load(part + k * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   red[f][j] = t;  // red is free again: every thread passed the barriers above

@@ -11,7 +11,7 @@ tail -8 gpurun_out/r03b_tune_stats.log
 MODE=awq timeout -k 10 300 python scripts/tune_fast.py $T/libqz_base.so $T/libqz_new.so > gpurun_out/r03b_tune_fq.log 2>&1 \
   || { tail -20 gpurun_out/r03b_tune_fq.log; exit 1; }
 tail -8 gpurun_out/r03b_tune_fq.log
-[ "${PROBE:-1}" = 1 ] || exit 0
+[ "${PROBE:-0}" = 1 ] || exit 0  # the probe ran once (profiles/r03b_bmm_probe.log)
 timeout -k 10 120 python -u scripts/bmm_fault_probe.py > gpurun_out/r03b_bmm_probe.log 2>&1
 echo "probe rc=$?"
 tail -20 gpurun_out/r03b_bmm_probe.log
