@@ -52,6 +52,26 @@ from .quantization import QuantizationArgs
 from .recipe import AWQMapping
 
 log = logging.getLogger(__name__)
+
+PHASE_TIMING = os.environ.get("QZ_AWQ_PHASE_TIMING", "0") == "1"  # diagnostics: synchronised per-phase wall times
+PHASES: Dict[str, float] = {}  # phase name -> seconds, accumulated while PHASE_TIMING
+
+
+@contextlib.contextmanager
+def phase(name: str):
+    """Accumulate the synchronised wall time of a block under ``name`` (QZ_AWQ_PHASE_TIMING=1
+    only: the synchronisations perturb the overlap they measure, so it is a diagnostic mode)."""
+    if not PHASE_TIMING:
+        yield
+        return
+    import time
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    try:
+        yield
+    finally:
+        torch.cuda.synchronize()
+        PHASES[name] = PHASES.get(name, 0.0) + time.perf_counter() - t0
 _D9_LOGGED: set = set()  # (layer class, balance suffix) pairs already reported at INFO
 
 # llmcompressor's default mappings for Llama/Qwen-style decoder blocks
@@ -662,6 +682,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             experts[id(r.balance[0].module)] = _ExpertInputs(r.balance[0].module, calibrate_all_experts)
             hooks.append(experts[id(r.balance[0].module)])
     stacked = stack_layer_calls(layer_inputs) if batched_calls else None
+    calib = phase("calibration pass")
+    calib.__enter__()
     try:
         if stacked is not None:  # one batched call; the hooks split it back into the samples
             _SAMPLES[0] = len(layer_inputs)
@@ -675,6 +697,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     finally:
         for h in hooks:
             h.remove()
+        calib.__exit__(None, None, None)
     for ei in experts.values():
         ei.snapshot()
     n_batches = len(layer_inputs)
@@ -864,20 +887,25 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     report: Dict[str, Any] = {}
     for batch in _independent_batches(resolved):
         if len(batch) == 1:
-            apply(batch[0], search(batch[0], grid_shard=True))
+            r0 = batch[0]
+            kind = ("grid, MoE-block parent" if r0.parent_kind == "module" and all(b.index is not None for b in r0.balance)
+                    else f"grid, {r0.parent_kind} parent")
+            with phase(kind):
+                apply(r0, search(r0, grid_shard=True))
             continue
         # mutually independent single-layer-parent mappings (e.g. every expert's w3 -> w2):
         # search all (sharded over ranks under torch.distributed), then smooth in order
         stateful = stateful_observers and any(quantized[r.balance_names[0]].observer in STATEFUL_OBSERVERS
                                               for r in batch)
-        if not stateful and _expert_batchable(batch, quantized, calibrate_all_experts):
-            b0 = batch[0].balance[0]
-            ei = experts[id(b0.module)]
-            n_tok = sum(x.shape[0] for x in ei.x)
-            w2 = getattr(b0.module, b0.param_name)
-            found = _sharded_search(batch, search_experts, _expert_chunk(n_tok, w2.shape[2], w2.shape[1]), n_grid)
-        else:
-            found = _sharded_search(batch, lambda c: [search(c[0])], 1, n_grid)
-        for r, f in zip(batch, found):
-            apply(r, f)
+        with phase("expert searches"):
+            if not stateful and _expert_batchable(batch, quantized, calibrate_all_experts):
+                b0 = batch[0].balance[0]
+                ei = experts[id(b0.module)]
+                n_tok = sum(x.shape[0] for x in ei.x)
+                w2 = getattr(b0.module, b0.param_name)
+                found = _sharded_search(batch, search_experts, _expert_chunk(n_tok, w2.shape[2], w2.shape[1]), n_grid)
+            else:
+                found = _sharded_search(batch, lambda c: [search(c[0])], 1, n_grid)
+            for r, f in zip(batch, found):
+                apply(r, f)
     return report

@@ -144,20 +144,23 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
                                 stateful_observers=stateful_observers, batched_calls=batched)
         report[f"{lname}.{i}"] = rep
         stacked = awq_mod.stack_layer_calls(inputs) if batched else None
-        if stacked is not None:  # propagate all samples in one call, split back per sample
-            out = _layer_out(layer(*stacked[0], **stacked[1]))
-            nxt = [((out[j:j + 1],) + tuple(args[1:]), kwargs) for j, (args, kwargs) in enumerate(inputs)]
-        else:
-            nxt = []
-            for args, kwargs in inputs:
-                out = _layer_out(layer(*args, **kwargs))
-                nxt.append(((out,) + tuple(args[1:]), kwargs))
+        with awq_mod.phase("propagation"):
+            if stacked is not None:  # propagate all samples in one call, split back per sample
+                out = _layer_out(layer(*stacked[0], **stacked[1]))
+                nxt = [((out[j:j + 1],) + tuple(args[1:]), kwargs) for j, (args, kwargs) in enumerate(inputs)]
+            else:
+                nxt = []
+                for args, kwargs in inputs:
+                    out = _layer_out(layer(*args, **kwargs))
+                    nxt.append(((out,) + tuple(args[1:]), kwargs))
         inputs = nxt
         if residency is not None:  # the other ranks keep only the tensors of their own shards
             residency.release(layer)
         if host is not None:
             _offload(layer, host)
         log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), time.time() - t0)
+        if awq_mod.PHASE_TIMING:
+            log.info("AWQ phases so far (s): %s", {k: round(v, 3) for k, v in awq_mod.PHASES.items()})
 
 
 def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, processor=None,
