@@ -40,6 +40,7 @@ import contextlib
 import logging
 import os
 import re
+import threading
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -212,15 +213,82 @@ def stack_layer_calls(layer_inputs: List[Tuple[tuple, dict]]) -> Optional[Tuple[
     return (torch.cat([a[0] for a, _ in layer_inputs], dim=0),) + tuple(a0[1:]), dict(k0)
 
 
+# ------------------------------------------------------------------ concurrent sample calls
+CALIB_THREADS = int(os.environ.get("QZ_CALIB_THREADS", "1"))  # per-sample layer calls on N host threads / streams
+_SLOT = threading.local()  # .j = the calibration sample the current thread's layer call belongs to
+_calib_streams: Dict[Tuple[str, int], List] = {}
+
+
+def _slot() -> Optional[int]:
+    return getattr(_SLOT, "j", None)
+
+
+def run_samples(fn: Callable[[int], Any], n: int, threads: int = 0) -> List[Any]:
+    """``[fn(j) for j in range(n)]`` -- with ``threads`` > 1 (default ``QZ_CALIB_THREADS``) the
+    calls run on that many host threads, each enqueueing on its own stream (sample j on thread
+    j % threads), so one sample's host work and syncs (the MoE blocks' routing reads) overlap
+    the others' kernels.  Every call computes exactly what it would alone; the hooks below file
+    what they see under the sample index (``_SLOT``) and ``finish()`` combines it in sample
+    order, so the results are bit-identical to the sequential calls."""
+    threads = threads or CALIB_THREADS
+    if threads <= 1 or n < 2 or not torch.cuda.is_available():
+        return [fn(j) for j in range(n)]
+    main = torch.cuda.current_stream()
+    dev = main.device
+    key = (str(dev), threads)
+    if key not in _calib_streams:
+        _calib_streams[key] = [torch.cuda.Stream(dev) for _ in range(threads)]
+    streams = _calib_streams[key]
+    for st in streams:
+        st.wait_stream(main)
+    out: List[Any] = [None] * n
+    errs: List[BaseException] = []
+
+    def worker(t: int):
+        try:
+            with torch.cuda.device(dev), torch.cuda.stream(streams[t]), torch.no_grad():
+                for j in range(t, n, threads):
+                    if errs:
+                        return
+                    _SLOT.j = j
+                    out[j] = fn(j)
+        except BaseException as e:  # noqa: BLE001 -- re-raised in the caller
+            errs.append(e)
+        finally:
+            _SLOT.j = None
+
+    ths = [threading.Thread(target=worker, args=(t,), name=f"qz-calib-{t}") for t in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    for st in streams:
+        main.wait_stream(st)
+    if errs:
+        raise errs[0]
+    return out
+
+
 class _ParentCache:
     """Forward pre-hook on a parent module: cache its (args, kwargs) per calibration batch."""
 
     def __init__(self, module: nn.Module):
         self.calls: List[Tuple[tuple, dict]] = []
+        self.slots: Dict[int, List[Tuple[tuple, dict]]] = {}
         self.h = module.register_forward_pre_hook(self._hook, with_kwargs=True)
 
     def _hook(self, mod, args, kwargs):
-        self.calls.append((tuple(a.detach() if torch.is_tensor(a) else a for a in args), dict(kwargs)))
+        call = (tuple(a.detach() if torch.is_tensor(a) else a for a in args), dict(kwargs))
+        j = _slot()
+        if j is None:
+            self.calls.append(call)
+        else:
+            self.slots.setdefault(j, []).append(call)
+
+    def finish(self):
+        for j in sorted(self.slots):
+            self.calls.extend(self.slots[j])
+        self.slots = {}
 
     def remove(self):
         self.h.remove()
@@ -232,11 +300,29 @@ class _AbsMean:
     def __init__(self, module: Optional[nn.Module] = None):
         self.sum = None
         self.count = 0
+        self.slots: Dict[int, List[Tuple[torch.Tensor, int]]] = {}
         self.h = module.register_forward_pre_hook(self._hook) if module is not None else None
 
     def _hook(self, mod, args):
+        j = _slot()
         for x in _split_samples(args[0]):  # one add per calibration sample, as per-sample calls did
-            self.add(x)
+            if j is None:
+                self.add(x)
+            elif x.numel():  # concurrent samples: this sample's total alone, added in order by finish()
+                part = torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device)
+                self.slots.setdefault(j, []).append((part, ops.awq_absmean_accum(x.detach(), part)))
+
+    def finish(self):
+        """sum = ((0 + t_0) + t_1) + ... over the samples in order: the kernel adds each call's
+        total to sum[c] with one f32 add, so adding the per-sample totals (each 0 + t_j = t_j)
+        in sample order gives the sequential calls' bits."""
+        for j in sorted(self.slots):
+            for part, n in self.slots[j]:
+                if self.sum is None:
+                    self.sum = torch.zeros_like(part)
+                self.sum += part
+                self.count += n
+        self.slots = {}
 
     def add(self, x: torch.Tensor):
         if self.sum is None:
@@ -263,13 +349,26 @@ class _ExpertInputs:
         self.topk: List[Optional[torch.Tensor]] = []
         self.gate_up0: Optional[torch.Tensor] = None  # pre-smoothing snapshot
         self._xcat: Optional[torch.Tensor] = None  # every batch's tokens, concatenated (lazily)
+        self.slots: Dict[int, Tuple[list, list]] = {}
         self.h = module.register_forward_pre_hook(self._hook)
 
     def _hook(self, mod, args):
         xs = _split_samples(args[0].detach())
         tk = _split_samples(args[1].detach()) if len(args) > 1 and torch.is_tensor(args[1]) else [None] * len(xs)
-        self.x.extend(xs)
-        self.topk.extend(tk)
+        j = _slot()
+        if j is None:
+            self.x.extend(xs)
+            self.topk.extend(tk)
+        else:
+            sx, st = self.slots.setdefault(j, ([], []))
+            sx.extend(xs)
+            st.extend(tk)
+
+    def finish(self):
+        for j in sorted(self.slots):
+            self.x.extend(self.slots[j][0])
+            self.topk.extend(self.slots[j][1])
+        self.slots = {}
 
     def remove(self):
         self.h.remove()
@@ -692,12 +791,13 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             finally:
                 _SAMPLES[0] = 0
         else:
-            for args, kwargs in layer_inputs:
-                layer(*args, **kwargs)
+            run_samples(lambda j: (layer(*layer_inputs[j][0], **layer_inputs[j][1]), None)[1], len(layer_inputs))
     finally:
         for h in hooks:
             h.remove()
         calib.__exit__(None, None, None)
+    for h in hooks:
+        h.finish()
     for ei in experts.values():
         ei.snapshot()
     n_batches = len(layer_inputs)

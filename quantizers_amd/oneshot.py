@@ -148,11 +148,9 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
             if stacked is not None:  # propagate all samples in one call, split back per sample
                 out = _layer_out(layer(*stacked[0], **stacked[1]))
                 nxt = [((out[j:j + 1],) + tuple(args[1:]), kwargs) for j, (args, kwargs) in enumerate(inputs)]
-            else:
-                nxt = []
-                for args, kwargs in inputs:
-                    out = _layer_out(layer(*args, **kwargs))
-                    nxt.append(((out,) + tuple(args[1:]), kwargs))
+            else:  # per sample (on QZ_CALIB_THREADS host threads / streams when set; same bits)
+                outs = awq_mod.run_samples(lambda j: _layer_out(layer(*inputs[j][0], **inputs[j][1])), len(inputs))
+                nxt = [((out,) + tuple(args[1:]), kwargs) for out, (args, kwargs) in zip(outs, inputs)]
         inputs = nxt
         if residency is not None:  # the other ranks keep only the tensors of their own shards
             residency.release(layer)

@@ -757,3 +757,30 @@ def test_dense_awq_grid_split_three_ranks(cuda, tmp_path):
     other = torch.load(out, weights_only=True)
     for k, v in m.state_dict().items():
         _eq(v, other[k], k)
+
+
+@pytest.mark.parametrize("arch", ["qwen3", "qwen3_moe", "minimax"])
+def test_concurrent_sample_calls_bit_identical(cuda, monkeypatch, arch):
+    """QZ_CALIB_THREADS: the per-sample calibration and propagation calls on 3 host threads /
+    streams (the hooks file their observations per sample and combine them in sample order)
+    give the loss histories and smoothed parameters of the sequential calls, bit for bit."""
+    import quantizers_amd.awq as awq_mod
+    import quantizers_amd.oneshot as os_mod
+    build = {"qwen3": _qwen3, "qwen3_moe": _qwen3_moe, "minimax": _minimax}[arch]
+    recipe = os.path.join(ROOT, "configs", "recipes",
+                          {"qwen3": "awq_w4a16_g32.yaml", "qwen3_moe": "awq_w4a16_g32.yaml",
+                           "minimax": "minimax_awq_mixedprec.yaml"}[arch])
+    monkeypatch.setattr(os_mod, "BATCH_LAYER_CALLS", False)  # the per-sample path is what runs threaded
+    out = {}
+    for threads in (1, 3):
+        monkeypatch.setattr(awq_mod, "CALIB_THREADS", threads)
+        m = build().to(cuda)
+        oneshot(m, recipe, dataset=_calib(n=5, vocab=256), max_seq_length=64)
+        out[threads] = (m.awq_report, {n: p.detach().clone() for n, p in m.named_parameters()})
+    (r1, p1), (r3, p3) = out[1], out[3]
+    assert r1.keys() == r3.keys()
+    for layer in r1:
+        for smooth, r in r1[layer].items():
+            assert r.get("history") == r3[layer][smooth].get("history"), (layer, smooth)
+    for n in p1:
+        _eq(p1[n], p3[n], n)
