@@ -18,6 +18,7 @@ namespace {
 constexpr int WAVE = 64;
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+__device__ __forceinline__ int64_t cdiv_d(int64_t a, int64_t b) { return (a + b - 1) / b; }
 inline bool aligned(const void* p, size_t n) { return ((uintptr_t)p % n) == 0; }
 int launch_err() {
   hipError_t e = hipGetLastError();
@@ -145,22 +146,30 @@ __global__ __launch_bounds__(FW * 64) void k_colsum_final(const T* part, int64_t
 }
 
 // ---------------------------------------------- a3 / a4 in ONE launch (round 3)
-// Narrow column windows (WIN = 128 columns, or the group width when wider): a wave-load covers
-// RPW = 64 / (WIN / 8) rows of WIN columns (lane = 8 columns, 16-B loads, 256-B row segments), so
-// a [rows, C] matrix splits into 4x more windows than with 512-column windows and the row chunks
-// can be 4x fewer for the same number of workgroups: the partial slab is small enough for the
-// LAST-ARRIVING workgroup of each window to reduce it inside the same launch (no second kernel,
-// no launch gap).  Arrival counters live at the head of the caller's workspace (STATS_CNT words,
-// zero before the first call; the last arriver resets its word, so every call leaves them zero).
-// Fixed order, hence deterministic: slot s = wave * RPW + (lane / (WIN / 8)) sums rows
-// r0 + s, r0 + s + S, ... (S = SWP * RPW slots) in order; a chunk's partial is
-// ((slot 0 + slot 1) + ...) + slot S-1; the final sum per column is, over TF = NT / WIN thread
-// groups f, ((sum_f=0 + sum_f=1) + ...) where sum_f adds chunks f, f + TF, ... in order.
+// Column windows of WIN columns (lane = 8 columns, 16-B loads; a wave-load covers RPW =
+// 64 / (WIN / 8) rows of WIN columns) x row chunks, as the two-launch kernels above, but the
+// chunk partials are reduced INSIDE the launch by the last-arriving workgroups: chunks form
+// groups of CPG; the last workgroup of a group to finish sums the group's partials (fixed
+// order) into a group partial, and the last group to finish sums the group partials into
+// sum[c].  No second kernel, no launch gap, and each reducing workgroup reads only CPG (or G)
+// rows of the window.  Arrival counters live at the head of the caller's workspace (STATS_CNT
+// words, zero before the first call; every last arriver resets its word, so every call leaves
+// them zero).  Fixed order, hence deterministic: slot s = wave * RPW + (lane / (WIN / 8)) sums
+// rows r0 + s, r0 + s + S, ... (S = SWP * RPW slots) in order; a chunk partial is
+// ((slot 0 + slot 1) + ...) + slot S-1; a group partial and the final sum are each, over TF =
+// NT / WIN thread groups f, ((sum_f=0 + sum_f=1) + ...) where sum_f adds items f, f + TF, ... of
+// the group (chunks) / of the groups, in order.
 constexpr int STATS_CNT = 8192;  // arrival counters (uint32) at the head of a statistics workspace
 constexpr int64_t STATS_HEAD = (int64_t)STATS_CNT * 4;
 static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics workspace (quantizers_amd.h)");
 #ifndef QZ_STATS_1L
 #define QZ_STATS_1L 1  // 1: one-launch statistics; 0: the two-launch kernels above (A/B knob)
+#endif
+#ifndef QZ_STATS_CPG
+#define QZ_STATS_CPG 8  // tuning knob: chunks per first-level reduction group
+#endif
+#ifndef QZ_ABS1_WIN
+#define QZ_ABS1_WIN 512  // tuning knob: absmean column window (128 / 256 / 512)
 #endif
 #ifndef QZ_ABS1_WPB
 #define QZ_ABS1_WPB 8
@@ -172,61 +181,134 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #define QZ_ABS1_BLOCKS 1024  // tuning knob: target workgroups of the one-launch absmean
 #endif
 #ifndef QZ_ABS1_MIN_RC
-#define QZ_ABS1_MIN_RC 256  // tuning knob: minimum tokens per chunk
+#define QZ_ABS1_MIN_RC 128  // tuning knob: minimum tokens per chunk
+#endif
+#ifndef QZ_WM1_WIN
+#define QZ_WM1_WIN 512  // tuning knob: w_mean column window (at least the group size)
 #endif
 #ifndef QZ_WM1_WPB
 #define QZ_WM1_WPB 8
+#endif
+#ifndef QZ_WM1_PP
+#define QZ_WM1_PP 1  // tuning knob: w_mean walk with two register sets in turn
+#endif
+#ifndef QZ_ABS1_PP
+#define QZ_ABS1_PP 0  // tuning knob: absmean walk with two register sets in turn
 #endif
 #ifndef QZ_WM1_NB
 #define QZ_WM1_NB 4
 #endif
 #ifndef QZ_WM1_BLOCKS
-#define QZ_WM1_BLOCKS 512  // tuning knob: target workgroups of the one-launch w_mean
+#define QZ_WM1_BLOCKS 256  // tuning knob: target workgroups of the one-launch w_mean
 #endif
 #ifndef QZ_WM1_MIN_RC
-#define QZ_WM1_MIN_RC 128  // tuning knob: minimum rows per chunk
+#define QZ_WM1_MIN_RC 16  // tuning knob: minimum rows per chunk
 #endif
 
 // rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per
 // batch, the next batch loaded before the current one is used; f(v, valid) per row in order.  rb
-// is wave-uniform; the loop condition guarantees every row of a non-final batch is valid.
-template <int S, int SNB, typename F>
+// is wave-uniform; every row of a batch that is followed by another batch is valid.  PP: two
+// register sets used in turn (no copies between them, but the loop body twice: more VGPRs --
+// taken by w_mean, whose grid is 2 waves per SIMD anyway); otherwise the next batch is copied
+// into the current one (absmean: 8 waves per SIMD need the VGPRs).
+template <int S, int SNB, bool PP, typename F>
 __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int64_t rb, int q, int64_t r1, F&& f) {
   if (rb >= r1) return;
   const uint32_t rlast = (uint32_t)(r1 - 1), uld = (uint32_t)ld;
   auto ld16 = [&](int64_t r) {
     return *reinterpret_cast<const uint4*>(base + (uint64_t)std::min((uint32_t)r, rlast) * uld);
   };
-  uint4 cur[SNB];
+  constexpr int64_t STEP = (int64_t)SNB * S;
+  uint4 a[SNB], b[SNB];
 #pragma unroll
-  for (int j = 0; j < SNB; ++j) cur[j] = ld16(rb + q + (int64_t)j * S);
-  for (; rb + (int64_t)SNB * S < r1; rb += (int64_t)SNB * S) {
-    uint4 nxt[SNB];
+  for (int j = 0; j < SNB; ++j) a[j] = ld16(rb + q + (int64_t)j * S);
+  if constexpr (!PP) {
+    for (; rb + STEP < r1; rb += STEP) {
 #pragma unroll
-    for (int j = 0; j < SNB; ++j) nxt[j] = ld16(rb + q + (int64_t)(SNB + j) * S);
+      for (int j = 0; j < SNB; ++j) b[j] = ld16(rb + STEP + q + (int64_t)j * S);
 #pragma unroll
-    for (int j = 0; j < SNB; ++j) f(cur[j], true);
+      for (int j = 0; j < SNB; ++j) f(a[j], true);
 #pragma unroll
-    for (int j = 0; j < SNB; ++j) cur[j] = nxt[j];
+      for (int j = 0; j < SNB; ++j) a[j] = b[j];
+    }
+#pragma unroll
+    for (int j = 0; j < SNB; ++j) f(a[j], rb + q + (int64_t)j * S < r1);
+    return;
+  } else {
+    while (true) {
+      if (rb + STEP >= r1) {
+#pragma unroll
+        for (int j = 0; j < SNB; ++j) f(a[j], rb + q + (int64_t)j * S < r1);
+        return;
+      }
+#pragma unroll
+      for (int j = 0; j < SNB; ++j) b[j] = ld16(rb + STEP + q + (int64_t)j * S);
+#pragma unroll
+      for (int j = 0; j < SNB; ++j) f(a[j], true);
+      rb += STEP;
+      if (rb + STEP >= r1) {
+#pragma unroll
+        for (int j = 0; j < SNB; ++j) f(b[j], rb + q + (int64_t)j * S < r1);
+        return;
+      }
+#pragma unroll
+      for (int j = 0; j < SNB; ++j) a[j] = ld16(rb + STEP + q + (int64_t)j * S);
+#pragma unroll
+      for (int j = 0; j < SNB; ++j) f(b[j], true);
+      rb += STEP;
+    }
   }
-#pragma unroll
-  for (int j = 0; j < SNB; ++j) f(cur[j], rb + q + (int64_t)j * S < r1);
 }
 
-// combine the slots of this workgroup into part[chunk][c], then the window's last arriver sums
-// the chunks into sum[c] (see the order above) and resets the window's counter.
 // Memory ordering without a device-scope fence (an agent-scope release writes the whole L2 back
-// and serialised the first version: 0.25-0.35 us per workgroup, profiles/r03b_tune_stats_fence.log):
-// the partials are written with agent-coherent (sc1) stores, every thread waits for its own
-// stores to complete (s_waitcnt 0) before the workgroup barrier, thread 0 then arrives with a
-// relaxed agent-scope atomic, and the last arriver reads the partials with agent-coherent loads.
+// and serialised a first version: 0.25-0.35 us per workgroup, profiles/r03b_tune_stats_fence.log):
+// partials are written with agent-coherent (sc1) stores, every thread waits for its own stores
+// to complete (s_waitcnt 0) before the workgroup barrier, thread 0 then arrives with a relaxed
+// agent-scope atomic, and a last arriver reads the partials with agent-coherent loads.
 template <typename T>
 __device__ __forceinline__ void st_coherent(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// arrive at *c; true (on every thread) for the workgroup that completes `expect` arrivals
+__device__ __forceinline__ bool arrive_last(unsigned* c, unsigned expect) {
+  __shared__ int last;
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's coherent stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0) last = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == expect - 1;
+  __syncthreads();
+  const bool l = last;
+  if (l && threadIdx.x == 0) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return l;
+}
+// fixed-order sum of rows src[i * C + c], i < n, for the window's columns: thread (j, f) adds
+// rows f, f + TF, ... (coherent loads), then the TF sums are added in order; the result is valid
+// in the threads with f == 0 (t = threadIdx.x)
+template <int WIN, int NT, typename T>
+__device__ __forceinline__ T reduce_rows(T (*red)[WIN], const T* src, int64_t n, int64_t C, int64_t cb) {
+  constexpr int TF = NT / WIN;
+  const int j = threadIdx.x % WIN, f = threadIdx.x / WIN;
+  const int64_t c = cb + j;
+  T t = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int64_t i = f; i < n; i += TF) t += __hip_atomic_load(src + i * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if constexpr (TF == 1) {
+    return t;
+  } else {
+    __syncthreads();  // red may still be read by an earlier reduction
+    red[f][j] = t;
+    __syncthreads();
+    T u = red[0][j];
+#pragma unroll
+    for (int k = 1; k < TF; ++k) u += red[k][j];
+    return u;
+  }
+}
+
 template <int WIN, int SWP, typename T>
 __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int lane, int wv, int64_t C, int64_t nch,
-                                             T* part, unsigned* cnt, T* sum) {
+                                             int64_t cpg, T* part, T* gpart, unsigned* cnt, T* sum) {
   constexpr int LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, NT = SWP * 64, TF = NT / WIN;
   static_assert(TF >= 1 && NT % WIN == 0 && S >= TF, "stats window");
   const int q = lane / LPR, c8 = lane % LPR;
@@ -234,52 +316,43 @@ __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int la
   for (int i = 0; i < 8; ++i) red[wv * RPW + q][c8 * 8 + i] = acc[i];
   __syncthreads();
   const int64_t cb = (int64_t)blockIdx.x * WIN;
+  const int64_t k = blockIdx.y;
   for (int j = threadIdx.x; j < WIN; j += NT) {
     const int64_t c = cb + j;
     if (c < C) {
       T t = red[0][j];
 #pragma unroll
-      for (int k = 1; k < S; ++k) t += red[k][j];
-      st_coherent(part + (int64_t)blockIdx.y * C + c, t);
+      for (int s = 1; s < S; ++s) t += red[s][j];
+      st_coherent(part + k * C + c, t);
     }
   }
-  __shared__ int last;
-  __builtin_amdgcn_s_waitcnt(0);  // this thread's partial stores have completed
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nch - 1);
-  __syncthreads();
-  if (!last) return;
-  const int j = threadIdx.x % WIN, f = threadIdx.x / WIN;
-  const int64_t c = cb + j;
-  T t = 0;
-  if (c < C) {
-#pragma unroll 4
-    for (int64_t k = f; k < nch; k += TF)  // coherent loads: partials written on every XCD
-      t += __hip_atomic_load(part + k * C + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t ng = cdiv_d(nch, cpg), g = k / cpg, g0 = g * cpg;
+  const int64_t n_g = std::min<int64_t>(cpg, nch - g0);
+  unsigned* wc = cnt + blockIdx.x * (ng + 1);
+  if (!arrive_last(wc + g, (unsigned)n_g)) return;
+  const T vg = reduce_rows<WIN, NT>(red, part + g0 * C, n_g, C, cb);  // this group's chunks
+  const bool out_thread = threadIdx.x < WIN && cb + threadIdx.x < C;
+  if (ng == 1) {
+    if (out_thread) sum[cb + threadIdx.x] += vg;
+    return;
   }
-  red[f][j] = t;  // red is free again: every thread passed the barriers above
-  __syncthreads();
-  if (f == 0 && c < C) {
-    T u = red[0][j];
-#pragma unroll
-    for (int k = 1; k < TF; ++k) u += red[k][j];
-    sum[c] += u;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (out_thread) st_coherent(gpart + g * C + cb + threadIdx.x, vg);
+  if (!arrive_last(wc + ng, (unsigned)ng)) return;
+  const T v = reduce_rows<WIN, NT>(red, gpart, ng, C, cb);  // the groups, in order
+  if (out_thread) sum[cb + threadIdx.x] += v;
 }
 
 template <int WIN>
 __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
-                                                                int64_t tc, int64_t nch, float* part, unsigned* cnt,
-                                                                float* sum) {
+                                                                int64_t tc, int64_t nch, int64_t cpg, float* part,
+                                                                float* gpart, unsigned* cnt, float* sum) {
   constexpr int SWP = QZ_ABS1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW;
   __shared__ float red[S][WIN];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
   const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  stats_walk<S, QZ_ABS1_NB>(x + c0, ld, t0 + wv * RPW, q, t1, [&](const uint4 v, bool ok) {
+  stats_walk<S, QZ_ABS1_NB, QZ_ABS1_PP>(x + c0, ld, t0 + wv * RPW, q, t1, [&](const uint4 v, bool ok) {
     const uint32_t w[4] = {ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -287,13 +360,21 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
       acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
     }
   });
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, part, cnt, sum);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum);
+}
+
+typedef float qz_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 qz_bf16x2 __attribute__((ext_vector_type(2)));
+// bf16(v) as an f32 in one convert: v_cvt_pk_bf16_f32(0, v) puts bf16(v) in the high half over
+// a zero low half, which is the f32 value bf16(v) itself
+__device__ __forceinline__ float bfr1(float v) {
+  return __uint_as_float(__builtin_bit_cast(uint32_t, __builtin_convertvector((qz_f32x2){0.0f, v}, qz_bf16x2)));
 }
 
 template <int WIN, int LOGL>
 __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w, int64_t R, int64_t C, int64_t ld,
-                                                             int64_t rc, int64_t nch, double* part, unsigned* cnt,
-                                                             double* wsum) {
+                                                             int64_t rc, int64_t nch, int64_t cpg, double* part,
+                                                             double* gpart, unsigned* cnt, double* wsum) {
   constexpr int SWP = QZ_WM1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, L = 1 << LOGL;
   static_assert(L <= LPR, "a group must lie inside one row segment of the window");
   __shared__ double red[S][WIN];
@@ -301,20 +382,20 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
   const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  stats_walk<S, QZ_WM1_NB>(w + c0, ld, r0 + wv * RPW, q, r1, [&](const uint4 v, bool ok) {
+  stats_walk<S, QZ_WM1_NB, QZ_WM1_PP>(w + c0, ld, r0 + wv * RPW, q, r1, [&](const uint4 v, bool ok) {
     const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
     // group absmax on |bf16| bit patterns (v_pk_max_u16 + DPP, every lane of the group on the same
     // row, so the group is uniformly valid or not), then |w| / bf16(amax + 1e-6)
     const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
     const float m = __uint_as_float(grp_max_u<L>(max(pm & 0xffffu, pm >> 16)) << 16);
-    const float rd = ok ? __builtin_amdgcn_rcpf(bfr(m + 1e-6f)) : 0.f;  // rcp lemma; 0: adds +0.0
+    const float rd = ok ? __builtin_amdgcn_rcpf(bfr1(m + 1e-6f)) : 0.f;  // rcp lemma; 0: adds +0.0
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      acc[2 * k] += (double)bfr(__uint_as_float(u[k] << 16) * rd);
-      acc[2 * k + 1] += (double)bfr(__uint_as_float(u[k] & 0xffff0000u) * rd);
+      acc[2 * k] += (double)bfr1(__uint_as_float(u[k] << 16) * rd);
+      acc[2 * k + 1] += (double)bfr1(__uint_as_float(u[k] & 0xffff0000u) * rd);
     }
   });
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, part, cnt, wsum);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum);
 }
 
 // chunking of the one-launch kernels: >= min_rc rows per chunk, about `blocks` workgroups
@@ -324,7 +405,15 @@ int64_t stats1_chunks(int64_t R, int64_t C, int win, int64_t blocks, int64_t min
   *rc = cdiv(R, n);
   return cdiv(R, *rc);
 }
-int wmean_win(int64_t g) { return (int)std::max<int64_t>(128, g); }
+int wmean_win(int64_t g) { return (int)std::min<int64_t>(512, std::max<int64_t>(QZ_WM1_WIN, g)); }
+constexpr int ABS1_WIN = QZ_ABS1_WIN;
+// workspace bytes of a one-launch statistics call: counters | chunk partials | group partials
+int64_t stats1_bytes(int64_t nch, int64_t C, int64_t elem) {
+  return STATS_HEAD + elem * (nch + cdiv(nch, QZ_STATS_CPG)) * C;
+}
+bool stats1_counters_fit(int64_t C, int win, int64_t nch) {
+  return cdiv(C, win) * (cdiv(nch, QZ_STATS_CPG) + 1) <= STATS_CNT;
+}
 
 // ----------------------------------------------- a5: grid-search loss sum((a - b)^2)
 // [3P] llmcompressor _compute_loss over a parent's outputs: (fp16_out - q_out) in the output
@@ -601,16 +690,20 @@ bool v8_ok(const void* w, int64_t C, int64_t ld, const float* s, bool cols) {
 
 extern "C" {
 
-static bool absmean_1l(int64_t channels) { return QZ_STATS_1L && cdiv(channels, 128) <= STATS_CNT; }
+// one-launch plan of an absmean call (chunks), or -1 when the counters do not fit (two-launch path)
+static int64_t absmean_1l(int64_t tokens, int64_t channels, int64_t* tc) {
+  if (!QZ_STATS_1L) return -1;
+  const int64_t n1 = stats1_chunks(tokens, channels, ABS1_WIN, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, tc);
+  return stats1_counters_fit(channels, ABS1_WIN, n1) ? n1 : -1;
+}
 
 size_t qz_awq_absmean_workspace_size(int64_t tokens, int64_t channels) {
   if (tokens <= 0 || channels <= 0) return 0;
-  int64_t tc;
+  int64_t tc, tc1;
   const int64_t nch = absmean_chunks(tokens, channels, &tc);  // the two-launch path's slab
-  if (absmean_1l(channels)) {  // (that path still serves unaligned inputs, after the counters)
-    const int64_t n1 = stats1_chunks(tokens, channels, 128, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &tc);
-    return (size_t)STATS_HEAD + (size_t)4 * (size_t)(std::max(n1, nch) * channels);
-  }
+  const int64_t n1 = absmean_1l(tokens, channels, &tc1);
+  if (n1 > 0)  // (the two-launch path still serves unaligned inputs, after the counters)
+    return (size_t)std::max<int64_t>(stats1_bytes(n1, channels, 4), STATS_HEAD + 4 * nch * channels);
   return (size_t)4 * (size_t)(nch * channels);
 }
 
@@ -621,20 +714,20 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   if (tokens == 0) return QZ_OK;
   if (!workspace || workspace_bytes < qz_awq_absmean_workspace_size(tokens, channels)) return QZ_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
-  int64_t tc;
+  int64_t tc, tc1;
   const int64_t nch = absmean_chunks(tokens, channels, &tc);
+  const int64_t n1 = absmean_1l(tokens, channels, &tc1);
   float* part = (float*)workspace;
   const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16) &&
                   tokens < INT32_MAX && ld < INT32_MAX;
-  if (v8 && absmean_1l(channels)) {
-    int64_t rc1;
-    const int64_t n1 = stats1_chunks(tokens, channels, 128, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &rc1);
-    hipLaunchKernelGGL(k_absmean_1l<128>, dim3((unsigned)cdiv(channels, 128), (unsigned)n1), dim3(QZ_ABS1_WPB * 64),
-                       0, st, (const uint16_t*)x, tokens, channels, ld, rc1, n1,
-                       (float*)((char*)workspace + STATS_HEAD), (unsigned*)workspace, sum);
+  if (v8 && n1 > 0) {
+    float* p1 = (float*)((char*)workspace + STATS_HEAD);
+    hipLaunchKernelGGL(k_absmean_1l<ABS1_WIN>, dim3((unsigned)cdiv(channels, ABS1_WIN), (unsigned)n1),
+                       dim3(QZ_ABS1_WPB * 64), 0, st, (const uint16_t*)x, tokens, channels, ld, tc1, n1,
+                       (int64_t)QZ_STATS_CPG, p1, p1 + n1 * channels, (unsigned*)workspace, sum);
     return launch_err();
   }
-  if (absmean_1l(channels)) part = (float*)((char*)workspace + STATS_HEAD);  // same workspace layout
+  if (n1 > 0) part = (float*)((char*)workspace + STATS_HEAD);  // same workspace layout
   if (v8) {
     dim3 grid((unsigned)cdiv(channels, 512), (unsigned)nch);
     hipLaunchKernelGGL(k_absmean_partial_v8, grid, dim3(AWP * 64), 0, st, (const uint16_t*)x, tokens, channels, ld, tc, part);
@@ -726,16 +819,45 @@ int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part
   return launch_err();
 }
 
-static bool wmean_1l(int64_t cols, int64_t g) { return QZ_STATS_1L && cdiv(cols, wmean_win(g)) <= STATS_CNT; }
+// one-launch plan of a w_mean call (chunks), or -1 (two-launch / generic paths)
+static int64_t wmean_1l(int64_t rows, int64_t cols, int64_t g, int64_t* rc) {
+  if (!QZ_STATS_1L || g < 8 || g > 512 || (g & (g - 1))) return -1;
+  const int win = wmean_win(g);
+  const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, rc);
+  return stats1_counters_fit(cols, win, n1) ? n1 : -1;
+}
 
 size_t qz_awq_weight_mean_workspace_size(int64_t rows, int64_t cols, int32_t group_size) {
   if (rows <= 0 || cols <= 0 || group_size <= 0) return 0;
   int64_t rc;
-  if (wmean_1l(cols, group_size))
-    return (size_t)STATS_HEAD +
-           (size_t)8 * (size_t)(stats1_chunks(rows, cols, wmean_win(group_size), QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc) * cols);
+  const int64_t n1 = wmean_1l(rows, cols, group_size, &rc);
+  if (n1 > 0) return (size_t)stats1_bytes(n1, cols, 8);
   return (size_t)8 * (size_t)(wmean_chunks(rows, cols, &rc) * cols);
 }
+
+extern "C++" {
+template <int WIN>
+static void launch_wmean_1l(int logl, dim3 grid, dim3 blk, hipStream_t st, const uint16_t* wp, int64_t rows, int64_t cols,
+                            int64_t ld, int64_t rc, int64_t n1, double* p1, unsigned* cnt, double* wsum) {
+  double* gp = p1 + n1 * cols;
+  const int64_t cpg = QZ_STATS_CPG;
+  switch (logl) {
+    case 0: hipLaunchKernelGGL((k_wmean_1l<WIN, 0>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum); break;
+    case 1: hipLaunchKernelGGL((k_wmean_1l<WIN, 1>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum); break;
+    case 2: hipLaunchKernelGGL((k_wmean_1l<WIN, 2>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum); break;
+    case 3: hipLaunchKernelGGL((k_wmean_1l<WIN, 3>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum); break;
+    case 4: hipLaunchKernelGGL((k_wmean_1l<WIN, 4>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum); break;
+    case 5:
+      if constexpr (WIN >= 256)
+        hipLaunchKernelGGL((k_wmean_1l<WIN, 5>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum);
+      break;
+    default:
+      if constexpr (WIN >= 512)
+        hipLaunchKernelGGL((k_wmean_1l<WIN, 6>), grid, blk, 0, st, wp, rows, cols, ld, rc, n1, cpg, p1, gp, cnt, wsum);
+      break;
+  }
+}
+}  // extern "C++"
 
 int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t ld, int32_t group_size, double* wsum,
                              void* workspace, size_t workspace_bytes, qz_stream_t stream) {
@@ -752,22 +874,16 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const uint16_t* wp = (const uint16_t*)w;
-    if (wmean_1l(cols, g)) {
-      int64_t rc1;
+    int64_t rc1;
+    const int64_t n1 = wmean_1l(rows, cols, g, &rc1);
+    if (n1 > 0) {
       const int win = wmean_win(g);
-      const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc1);
       dim3 grid1((unsigned)cdiv(cols, win), (unsigned)n1), blk1(QZ_WM1_WPB * 64);
       double* p1 = (double*)((char*)workspace + STATS_HEAD);
       unsigned* cnt = (unsigned*)workspace;
-      switch (logl) {
-        case 0: hipLaunchKernelGGL((k_wmean_1l<128, 0>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        case 1: hipLaunchKernelGGL((k_wmean_1l<128, 1>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        case 2: hipLaunchKernelGGL((k_wmean_1l<128, 2>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        case 3: hipLaunchKernelGGL((k_wmean_1l<128, 3>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        case 4: hipLaunchKernelGGL((k_wmean_1l<128, 4>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        case 5: hipLaunchKernelGGL((k_wmean_1l<256, 5>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-        default: hipLaunchKernelGGL((k_wmean_1l<512, 6>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum); break;
-      }
+      if (win == 512) launch_wmean_1l<512>(logl, grid1, blk1, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum);
+      else if (win == 256) launch_wmean_1l<256>(logl, grid1, blk1, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum);
+      else launch_wmean_1l<128>(logl, grid1, blk1, st, wp, rows, cols, ld, rc1, n1, p1, cnt, wsum);
       return launch_err();
     }
     int64_t rc;
@@ -797,26 +913,27 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
 int qz_awq_stats_layout(int32_t which, int64_t rows, int64_t cols, int32_t group_size, int64_t* out) {
   if (!out) return QZ_ERR_NULL;
   if (rows <= 0 || cols <= 0 || (which != 0 && which != 1) || (which == 1 && group_size <= 0)) return QZ_ERR_SHAPE;
-  const bool one = which == 0 ? absmean_1l(cols) : (wmean_1l(cols, group_size) && group_size >= 8 &&
-                                                   group_size <= 512 && (group_size & (group_size - 1)) == 0);
   int64_t rc = 0, nch = 0;
+  const int64_t n1 = which == 0 ? absmean_1l(rows, cols, &rc) : wmean_1l(rows, cols, group_size, &rc);
   int win = 512, swp = which == 0 ? AWP : WWP, tf = FW;
-  if (one) {
-    win = which == 0 ? 128 : wmean_win(group_size);
+  int64_t cpg = 0;
+  if (n1 > 0) {
+    nch = n1;
+    win = which == 0 ? ABS1_WIN : wmean_win(group_size);
     swp = which == 0 ? QZ_ABS1_WPB : QZ_WM1_WPB;
-    nch = which == 0 ? stats1_chunks(rows, cols, win, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, &rc)
-                     : stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, &rc);
     tf = swp * 64 / win;
+    cpg = QZ_STATS_CPG;
   } else {
     nch = which == 0 ? absmean_chunks(rows, cols, &rc) : wmean_chunks(rows, cols, &rc);
   }
-  out[0] = one;
+  out[0] = n1 > 0;
   out[1] = win;
   out[2] = rc;
   out[3] = nch;
   out[4] = (int64_t)swp * 64 / (win / 8);  // row slots per workgroup
   out[5] = tf;
-  out[6] = one ? STATS_HEAD : 0;
+  out[6] = n1 > 0 ? STATS_HEAD : 0;
+  out[7] = cpg;  // chunks per first-level group (0: the two-launch plan)
   return QZ_OK;
 }
 

@@ -77,10 +77,10 @@ def stats_workspace(nbytes: int, device) -> torch.Tensor:
 def awq_stats_layout(which: str, rows: int, cols: int, group_size: int = 0) -> Dict[str, int]:
     """The fixed summation plan of awq_absmean_accum (``which="absmean"``, rows = tokens) or
     awq_weight_mean_accum (``"wmean"``) for a [rows, cols] input (qz_awq_stats_layout)."""
-    out = (ctypes.c_int64 * 7)()
+    out = (ctypes.c_int64 * 8)()
     rc = _lib.load().qz_awq_stats_layout(0 if which == "absmean" else 1, rows, cols, int(group_size), out)
     _lib.check(rc, "qz_awq_stats_layout")
-    return dict(zip(("one_launch", "window", "rows_per_chunk", "chunks", "slots", "final_groups", "head_bytes"),
+    return dict(zip(("one_launch", "window", "rows_per_chunk", "chunks", "slots", "final_groups", "head_bytes", "chunks_per_group"),
                     list(out)))
 
 

@@ -8,9 +8,11 @@ as are the weights they read.
 Result on MI355X (profiles/r02a_guard_band.txt): canaries, inputs and per-slice outputs all
 intact after the batched kernels (synchronised and checked), and the NEXT call -- torch.bmm of
 a fresh bf16 [16, 2048, 768] tensor with these outputs transposed -- raised
-hipErrorIllegalAddress.  The fault is in the library batched GEMM at that shape, not in these
-kernels; the product's expert search uses one 2-D GEMM per expert (awq.search_experts), which
-the test runs instead."""
+hipErrorIllegalAddress.  Round 3 reproduced that fault with the same torch.bmm on plain
+allocations in a process that never loaded this library (scripts/bmm_fault_probe.py stage A,
+profiles/r03b_bmm_probe.log): a defect of torch's bundled hipBLASLt at that shape (DESIGN.md
+§9).  The product's expert search uses one 2-D GEMM per expert (awq.search_experts), which the
+test runs instead."""
 import ctypes
 
 import pytest

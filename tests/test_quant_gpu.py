@@ -287,7 +287,8 @@ def test_absmean_ragged_windows(cuda, tokens, ch):
 
 
 @pytest.mark.parametrize("rows,cols,g", [(1, 32, 32), (9, 96, 32), (45, 640, 128), (1001, 1088, 64),
-                                         (700, 1024, 256), (300, 2048, 512), (5000, 136, 8)])
+                                         (700, 1024, 256), (300, 2048, 512), (5000, 136, 8), (11008, 4096, 128),
+                                         (40000, 512, 32)])
 def test_weight_mean_ragged_windows(cuda, rows, cols, g):
     """w_mean with a partly empty last column window, row counts that are not multiples of the
     row slots per workgroup, and every window width (128 / 256 / 512 columns): the fixed-order
@@ -299,15 +300,17 @@ def test_weight_mean_ragged_windows(cuda, rows, cols, g):
 
 
 def _stats_tree(v, lay, dtype=None) -> "np.ndarray":
-    """Fixed-order restatement of the AWQ statistics reduction (ops.awq_stats_layout, f64 terms
-    ``v`` [R, C]).  One-launch plan: per row chunk, slot s sums rows s, s + S, ... in order, the
-    chunk partial is ((slot 0 + slot 1) + ...); the window's last workgroup then sums, for each of
-    the TF thread groups f, chunks f, f + TF, ... in order and adds the TF sums in order.  The
-    two-launch plan (wide channel counts) is the same with S = waves per workgroup and TF = 16."""
+    """Fixed-order restatement of the AWQ statistics reduction (ops.awq_stats_layout, terms ``v``
+    [R, C]).  Per row chunk, slot s sums rows s, s + S, ... in order and the chunk partial is
+    ((slot 0 + slot 1) + ...).  One-launch plan: chunks form groups of CPG; a group's partial and
+    then the final sum (over the groups; skipped with one group) are each, over TF thread
+    groups f, ((sum_0 + sum_1) + ...) where sum_f adds items f, f + TF, ... in order.  Two-launch
+    plan: the final sum alone, over all chunks, with TF = 16."""
     import numpy as np
     R, C = v.shape
     dt = v.dtype if dtype is None else dtype
-    rc, nch, S, TF = lay["rows_per_chunk"], lay["chunks"], lay["slots"], lay["final_groups"]
+    rc, nch, S, TF, cpg = (lay["rows_per_chunk"], lay["chunks"], lay["slots"], lay["final_groups"],
+                           lay["chunks_per_group"])
     part = np.zeros((nch, C), dtype=dt)
     for k in range(nch):
         r0, r1 = k * rc, min(R, (k + 1) * rc)
@@ -318,19 +321,26 @@ def _stats_tree(v, lay, dtype=None) -> "np.ndarray":
                 acc = acc + v[r]
             t = acc if t is None else t + acc
         part[k] = t
-    red = []
-    for f in range(TF):
-        acc = np.zeros(C, dtype=dt)
-        for k in range(f, nch, TF):
-            acc = acc + part[k]
-        red.append(acc)
-    t = red[0]
-    for f in range(1, TF):
-        t = t + red[f]
-    return np.zeros(C, dtype=dt) + t
+
+    def reduce(items):
+        red = []
+        for f in range(TF):
+            acc = np.zeros(C, dtype=dt)
+            for i in range(f, len(items), TF):
+                acc = acc + items[i]
+            red.append(acc)
+        t = red[0]
+        for f in range(1, TF):
+            t = t + red[f]
+        return t
+
+    if not cpg:
+        return np.zeros(C, dtype=dt) + reduce(list(part))
+    groups = [reduce(list(part[g:g + cpg])) for g in range(0, nch, cpg)]
+    return np.zeros(C, dtype=dt) + (groups[0] if len(groups) == 1 else reduce(groups))
 
 
-@pytest.mark.parametrize("tokens,ch", [(2048, 2560), (16384, 4096), (333, 1032), (7, 264)])
+@pytest.mark.parametrize("tokens,ch", [(2048, 2560), (16384, 4096), (333, 1032), (7, 264), (100000, 520)])
 def test_absmean_fixed_order_bit_exact(cuda, tokens, ch):
     """absmean's f32 sums equal the restated fixed-order tree bit for bit (one launch: the
     last-arriving workgroup of each window adds the chunk partials), and the statistics
