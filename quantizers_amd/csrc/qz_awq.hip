@@ -166,10 +166,10 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #define QZ_STATS_1L 1  // 1: one-launch statistics; 0: the two-launch kernels above (A/B knob)
 #endif
 #ifndef QZ_STATS_CPG
-#define QZ_STATS_CPG 8  // tuning knob: chunks per first-level reduction group
+#define QZ_STATS_CPG 32  // tuning knob: chunks per first-level reduction group
 #endif
 #ifndef QZ_ABS1_WIN
-#define QZ_ABS1_WIN 512  // tuning knob: absmean column window (128 / 256 / 512)
+#define QZ_ABS1_WIN 128  // tuning knob: absmean column window (128 / 256 / 512)
 #endif
 #ifndef QZ_ABS1_WPB
 #define QZ_ABS1_WPB 8
@@ -181,16 +181,16 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #define QZ_ABS1_BLOCKS 1024  // tuning knob: target workgroups of the one-launch absmean
 #endif
 #ifndef QZ_ABS1_MIN_RC
-#define QZ_ABS1_MIN_RC 128  // tuning knob: minimum tokens per chunk
+#define QZ_ABS1_MIN_RC 256  // tuning knob: minimum tokens per chunk
 #endif
 #ifndef QZ_WM1_WIN
-#define QZ_WM1_WIN 512  // tuning knob: w_mean column window (at least the group size)
+#define QZ_WM1_WIN 128  // tuning knob: w_mean column window (at least the group size)
 #endif
 #ifndef QZ_WM1_WPB
 #define QZ_WM1_WPB 8
 #endif
 #ifndef QZ_WM1_PP
-#define QZ_WM1_PP 1  // tuning knob: w_mean walk with two register sets in turn
+#define QZ_WM1_PP 0  // tuning knob: w_mean walk with two register sets in turn (same time, more VGPRs)
 #endif
 #ifndef QZ_ABS1_PP
 #define QZ_ABS1_PP 0  // tuning knob: absmean walk with two register sets in turn
@@ -202,7 +202,7 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #define QZ_WM1_BLOCKS 256  // tuning knob: target workgroups of the one-launch w_mean
 #endif
 #ifndef QZ_WM1_MIN_RC
-#define QZ_WM1_MIN_RC 16  // tuning knob: minimum rows per chunk
+#define QZ_WM1_MIN_RC 128  // tuning knob: minimum rows per chunk
 #endif
 
 // rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per

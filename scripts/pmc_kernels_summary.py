@@ -29,8 +29,8 @@ KERNELS = {
     "k_wmean_v8": ("AWQ w_mean stage 1", P * 2),
     "k_colsum_final<double>": ("AWQ w_mean stage 2", None),
     "k_scale_v8<true>": ("AWQ smoothing W[:, c] *= s[c]", P * 4 + C * 4),
-    "k_absmean_1l<128>": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
-    "k_wmean_1l<128, 4>": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
+    "k_absmean_1l<": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
+    "k_wmean_1l<": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
 }
 
 
