@@ -265,42 +265,67 @@ def _all_gather_into(out, inp):
         dist.all_gather_into_tensor(out, inp)
 
 
-def _event_us(fn, n, stream):
-    """Mean per-launch duration (HIP events on the launch stream) of fn(i), i = 0..n-1."""
-    for i in range(3):
-        fn(i)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
-    for i in range(n):
-        ev[i][0].record(stream)
-        fn(i)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    return sum(a.elapsed_time(b) for a, b in ev) / n * 1e3
-
-
-def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream):
+def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream, n=40):
     """The AWQ kernels on the headline weight shape, each with its
-    algorithmic bytes and achieved HBM GB/s (rotating the HBM-resident weight copies)."""
+    algorithmic bytes and achieved HBM GB/s (rotating the HBM-resident weight copies).
+
+    Each kernel is timed as ``n`` launches back to back between ONE pair of HIP events on the
+    launch stream, the C ABI called through pre-marshalled ctypes arguments (a few us of host
+    time per launch, less than a kernel), so the GPU never waits for the host: us = the steady
+    time per launch, including the gap between launches.  (Bracketing each launch with its own
+    event pair, as the round-2 bench did, also timed the GPU waiting for the next Python call.)"""
+    import ctypes
+    from quantizers_amd import _lib
+    lib = _lib.load()
+    P = ctypes.c_void_p
+    st = P(stream.cuda_stream)
     a = QuantizationArgs(num_bits=BITS, type="int", symmetric=True, group_size=GROUP)
+    ca = a.to_c()
     nc = len(copies)
     s = torch.rand(COLS, device=dev, generator=gen) + 0.5
     fq_out = torch.empty_like(copies[0])
+    fq_ws = ops.workspace(lib.qz_quantize_workspace_size(1, ROWS, COLS, ctypes.byref(ca)) + 256, dev)
     x = [(torch.randn(16384, COLS, device=dev, generator=gen)).to(torch.bfloat16) for _ in range(4)]
     sums = torch.zeros(COLS, dtype=torch.float32, device=dev)
     wsum = torch.zeros(COLS, dtype=torch.float64, device=dev)
+    with torch.cuda.stream(stream):
+        ws_a = ops.stats_workspace(lib.qz_awq_absmean_workspace_size(16384, COLS) + 256, dev)
+        ws_w = ops.stats_workspace(lib.qz_awq_weight_mean_workspace_size(ROWS, COLS, GROUP) + 256, dev)
+    wp = [P(c.data_ptr()) for c in copies]
+    xp = [P(t.data_ptr()) for t in x]
+
+    def ok(rc):
+        if rc:
+            _lib.check(rc, "bench awq kernel")
+
     res = {}
     for name, fn, nbytes in [
         ("fake_quant_scaled (a5: Q(W*s)/s, int4 g128)",
-         lambda i: ops.fake_quantize(copies[i % nc], a, col_scales=s, out=fq_out), PARAMS * 4 + COLS * 4),
+         lambda i: ok(lib.qz_awq_fake_quant(wp[i % nc], 1, ROWS, COLS, COLS, PARAMS, ctypes.byref(ca), P(s.data_ptr()),
+                                            P(fq_out.data_ptr()), P(fq_ws.data_ptr()), fq_ws.numel(), st)),
+         PARAMS * 4 + COLS * 4),
         ("absmean_accum (a3: sum|x| over [16384, 4096] activations)",
-         lambda i: ops.awq_absmean_accum(x[i % 4], sums), x[0].numel() * 2),
+         lambda i: ok(lib.qz_awq_absmean_accum(xp[i % 4], 16384, COLS, COLS, P(sums.data_ptr()), P(ws_a.data_ptr()),
+                                               ws_a.numel(), st)), x[0].numel() * 2),
         ("weight_mean_accum (a4: |W|/group absmax, g128)",
-         lambda i: ops.awq_weight_mean_accum(copies[i % nc], GROUP, wsum), PARAMS * 2),
+         lambda i: ok(lib.qz_awq_weight_mean_accum(wp[i % nc], ROWS, COLS, COLS, GROUP, P(wsum.data_ptr()),
+                                                   P(ws_w.data_ptr()), ws_w.numel(), st)), PARAMS * 2),
         ("scale_columns (a6: W[:, c] *= s[c])",
-         lambda i: ops.scale_columns_(copies[i % nc], s), PARAMS * 4),
+         lambda i: ok(lib.qz_scale_columns(wp[i % nc], ROWS, COLS, COLS, P(s.data_ptr()), i & 1, st)), PARAMS * 4),
     ]:
-        us = _event_us(fn, 40, stream)
-        res[name] = {"us": us, "alg_bytes": nbytes, "GBps": nbytes / (us * 1e-6) / 1e9}
+        for i in range(3):
+            fn(i)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(n):
+            fn(i)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / n
+        res[name] = {"us": us, "alg_bytes": nbytes, "GBps": nbytes / (us * 1e-6) / 1e9,
+                     "frac": nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                     "timing": f"{n} launches back to back between one event pair"}
     del x
     return res
 
