@@ -321,6 +321,32 @@ int qz_scale_columns(void* w, int64_t rows, int64_t cols, int64_t ld, const floa
 int qz_scale_rows(void* w, int64_t rows, int64_t cols, int64_t ld, const float* s,
                   int32_t divide, qz_stream_t stream);
 
+/*
+ * qz_moe_combine -- the tail of a fused-experts MoE forward in the eager arithmetic: for every
+ * token t, out[t, :] = (((+0 + v_0) + v_1) + ... + v_{k-1}) with a bf16 rounding after each
+ * add, where v_j = bf16(expert_out[r, :] * weights[perm[r]]) and r = src[t * top_k + j] is the
+ * expert-sorted row of t's j-th expert in ascending expert id.  expert_out is [rows, hidden]
+ * bf16 (rows = tokens * top_k), weights the flat routing weights [tokens * top_k] (bf16, or f32
+ * when weights_f32), perm / src int64 device arrays, out [tokens, hidden] bf16.  Replaces the
+ * per-expert `current * top_k_weights[...]` and bf16 `index_add_` of transformers' eager
+ * experts loop (transformers 4.57 modeling_qwen3_moe Qwen3MoeSparseMoeBlock.forward, as pinned
+ * by the reference's requirements) -- bit-identical to that loop.
+ */
+int qz_moe_combine(const void* expert_out, int64_t rows, int64_t hidden, const void* weights,
+                   int32_t weights_f32, const int64_t* perm, const int64_t* src, int64_t tokens,
+                   int32_t top_k, void* out, qz_stream_t stream);
+
+/*
+ * qz_moe_silu_mul -- out[r, c] = bf16(bf16(silu(gate_up[r, c])) * gate_up[r, inter + c]) for the
+ * [rows, 2 * inter] bf16 gate/up GEMM output (row stride ld >= 2 * inter) into a dense
+ * [rows, inter] bf16 out, with torch's silu arithmetic (x / (1 + exp(-x)) in f32).  Replaces
+ * `self.act_fn(gate) * up` of the eager experts loop (transformers 4.57
+ * modeling_qwen3_moe.Qwen3MoeMLP / the fused experts' forward); callers verify it against the
+ * composed ops on first use (the exp implementation is the device library's).
+ */
+int qz_moe_silu_mul(const void* gate_up, int64_t rows, int64_t inter, int64_t ld, void* out,
+                    qz_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,7 +31,8 @@ EXPORTS = (
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
     "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
-    "qz_awq_sq_err_partials_multi", "qz_awq_stats_layout",
+    "qz_awq_sq_err_partials_multi", "qz_awq_stats_layout", "qz_moe_combine",
+    "qz_moe_silu_mul",
 )
 
 
@@ -91,6 +92,8 @@ def load() -> ctypes.CDLL:
         "qz_awq_fake_quant_batched": ([P, I64, I64, I64, I64, I64, A, P, I64, P, P, SZ, P], ctypes.c_int),
         "qz_scale_columns": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
         "qz_scale_rows": ([P, I64, I64, I64, P, I32, P], ctypes.c_int),
+        "qz_moe_combine": ([P, I64, I64, P, I32, P, P, I64, I32, P, P], ctypes.c_int),
+        "qz_moe_silu_mul": ([P, I64, I64, I64, P, P], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():
         fn = getattr(lib, name)

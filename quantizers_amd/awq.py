@@ -407,6 +407,63 @@ EXPERT_MAJOR = os.environ.get("QZ_EXPERT_MAJOR", "1") == "1"  # expert searches:
 BATCHED_LOSS = os.environ.get("QZ_BATCHED_LOSS", "1") == "1"  # expert searches: one ordered reduce per search
 MULTI_LOSS = int(os.environ.get("QZ_MULTI_LOSS", "8"))  # expert searches: grid outputs per loss launch (<= 8)
 OVERLAP_LOSS = os.environ.get("QZ_OVERLAP_LOSS", "0") == "1"  # expert searches: loss kernels on a side stream (measured slower: off)
+GRID_GRAPHS = os.environ.get("QZ_GRID_GRAPHS", "0") == "1"  # MoE-block grids: forwards replayed from one HIP graph (r03i: replays ~10% faster, capture costs more: off)
+
+
+class _GraphedForward:
+    """The parent forward of a fixed-routing MoE-block grid, replayed from one HIP graph.
+
+    Every grid point re-runs the same MoE block on the same cached inputs, with the same
+    routing (``moe_eager.fixed_routing``) and the balance weights rewritten in place: the same
+    kernels on the same addresses each time.  Issued from Python that is ~260 launches per
+    forward (two GEMMs per routed expert on 4 streams), which the host cannot issue as fast as
+    the GPU runs them.  The first grid forward runs eagerly, is captured once (capture runs
+    nothing), replayed, and the replay's outputs are compared bit for bit with the eager ones;
+    on a match the remaining grid points replay the graph, otherwise (or when capture fails,
+    e.g. a host sync inside the forward) they run eagerly.  The outputs of a replay live in the
+    graph's buffers until the next replay, which is enqueued on the same stream after the loss
+    kernels that read them."""
+
+    def __init__(self, run: Callable[[], List[torch.Tensor]], name: str):
+        self.run, self.name = run, name
+        self.graph: Optional[Any] = None
+        self.outs: Optional[List[torch.Tensor]] = None
+        self.state: Optional[bool] = None  # None: not tried yet; True: replaying; False: eager
+
+    def __call__(self) -> List[torch.Tensor]:
+        if self.state:
+            self.graph.replay()
+            return self.outs
+        if self.state is False:
+            return self.run()
+        with phase("MoE-block grid: first forward, capture, check"):
+            return self._first()
+
+    def _first(self) -> List[torch.Tensor]:
+        want = self.run()
+        self.state = False
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                outs = self.run()
+            g.replay()
+            ok = len(outs) == len(want) and all(moe_eager._bits_equal(a, b) for a, b in zip(want, outs))
+        except RuntimeError as e:
+            log.info("AWQ: %s grid forward not capturable (%s); eager forwards", self.name, e)
+            return want
+        if ok:
+            self.graph, self.outs, self.state = g, outs, True
+        else:
+            log.info("AWQ: %s graph replay differs from the eager forward; eager forwards", self.name)
+        return want
+
+    def close(self) -> None:
+        """Release the graph once its last replay has finished: the executable graph owns the
+        runtime's side streams and argument buffers for its multi-stream replay, and its outputs
+        live in the graph's private memory pool."""
+        if self.graph is not None:
+            torch.cuda.synchronize()
+        self.graph = self.outs = None
 
 
 def _batched_losses(hs, ref_out, wq_all, losses) -> None:
@@ -869,6 +926,9 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         # by the grid, so the experts' routing is fixed across its forwards (moe_eager.fixed_routing)
         fixed = r.parent_kind == "module" and all(b.index is not None for b in r.balance)
         routing = moe_eager.fixed_routing() if fixed else contextlib.nullcontext()
+        graphed = None
+        if fixed and GRID_GRAPHS and x_mean.is_cuda:
+            run = graphed = _GraphedForward(run, r.smooth_name)
         with routing:
             for i in range(rank, n_grid, world):
                 ratio = i / n_grid
@@ -883,6 +943,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                         ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
                         _view(g).copy_(t)
                 losses[i] = _sq_err(ref_out, run())
+        if graphed is not None:
+            graphed.close()
         for g, w0 in zip(groups, orig):
             _view(g).copy_(w0)
         if world > 1:

@@ -10,8 +10,8 @@ of the outputs (``profiles/r02at_fast_eager.log``).
 
 ``FastEagerExperts`` computes the eager result with two grouped GEMMs (tokens sorted by expert:
 hipBLASLt gives every row the same bits as the per-expert GEMM), the routing weight, and k
-sequential bf16 adds in ascending expert order -- no host sync, ~10 launches instead of ~9 per
-expert.  The first call per input shape is checked bit for bit against the module's own eager
+sequential bf16 adds in ascending expert order -- on the GPU ``act(gate) * up`` as one
+qz_moe_silu_mul pass and the last three as one qz_moe_combine pass -- no host sync, ~10 launches instead of ~9 per expert.  The first call per input shape is checked bit for bit against the module's own eager
 forward; a mismatch makes that module use the eager forward for the rest of the pass.
 Decision D15: the AWQ pass runs MoE experts in this eager arithmetic."""
 from __future__ import annotations
@@ -25,10 +25,45 @@ from typing import Callable, Dict, Optional, Tuple
 import torch
 from torch import nn
 
+from . import ops
+
 log = logging.getLogger(__name__)
 
 FAST_EAGER = os.environ.get("QZ_FAST_EAGER_EXPERTS", "1") == "1"  # A/B knob: 0 = the eager loop itself
 PLANNED = os.environ.get("QZ_PLANNED_EXPERTS", "1") == "1"  # A/B knob: per-expert GEMMs from a grid's fixed routing
+FUSED_COMBINE = os.environ.get("QZ_MOE_FUSED_COMBINE", "1") == "1"  # A/B knob: qz_moe_combine for the weighted adds
+
+
+FUSED_ACT = os.environ.get("QZ_MOE_FUSED_ACT", "1") == "1"  # A/B knob: qz_moe_silu_mul for act_fn(gate) * up
+_ACT_OK: Dict[torch.device, bool] = {}  # qz_moe_silu_mul verified against the composed ops (per device)
+
+
+def _act_mul(m: nn.Module, gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``act_fn(gate) * up`` of the [rows, 2 * inter] gate/up GEMM output.  For a SiLU on bf16 GPU
+    tensors: one qz_moe_silu_mul pass instead of two strided ones -- compared bit for bit with
+    the composed ops on the first non-empty call per device (its exp is the device library's),
+    and never used again if they differ."""
+    gate, up = gu.chunk(2, dim=-1)
+    if (FUSED_ACT and gu.is_cuda and gu.dtype == torch.bfloat16 and gu.is_contiguous() and gu.numel()
+            and type(m.act_fn).__name__ in ("SiLUActivation", "SiLU") and not getattr(m.act_fn, "inplace", False)):
+        ok = _ACT_OK.get(gu.device)
+        if ok is None:
+            want = m.act_fn(gate) * up
+            ok = _ACT_OK[gu.device] = _bits_equal(ops.moe_silu_mul(gu), want)
+            if not ok:
+                log.info("MoE: qz_moe_silu_mul differs from the composed silu * up on %s; composed ops kept", gu.device)
+            return want if out is None else out.copy_(want)
+        if ok:
+            return ops.moe_silu_mul(gu, out=out)
+    return m.act_fn(gate) * up if out is None else torch.mul(m.act_fn(gate), up, out=out)
+
+
+def _fused(d: torch.Tensor, top_k_weights: torch.Tensor, hidden_states: torch.Tensor) -> bool:
+    """The weighting, reorder and k bf16 adds as one qz_moe_combine pass (same roundings, same
+    order: bit-identical to the composed ops, and checked against the eager loop like the rest of
+    this form); the composed PyTorch ops otherwise (CPU tensors, other dtypes)."""
+    return (FUSED_COMBINE and d.is_cuda and d.dtype == torch.bfloat16 and hidden_states.dtype == torch.bfloat16
+            and top_k_weights.dtype in (torch.bfloat16, torch.float32))
 
 
 def eager_forward(module: nn.Module) -> Optional[Callable]:
@@ -67,14 +102,18 @@ def fast_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Ten
         0, flat, torch.ones_like(flat))
     offs = counts.cumsum(0).to(torch.int32)
     xg = hidden_states[perm // k]
-    gate, up = nn.functional.grouped_mm(xg, m.gate_up_proj.transpose(-2, -1), offs=offs).chunk(2, dim=-1)
-    h = m.act_fn(gate) * up
+    h = _act_mul(m, nn.functional.grouped_mm(xg, m.gate_up_proj.transpose(-2, -1), offs=offs))
     d = nn.functional.grouped_mm(h, m.down_proj.transpose(-2, -1), offs=offs)
+    order = torch.argsort(top_k_index, dim=-1)  # each token's experts in ascending id: the eager add order
+    if _fused(d, top_k_weights, hidden_states):
+        inv = torch.empty_like(perm)
+        inv[perm] = torch.arange(perm.numel(), device=perm.device)
+        base = torch.arange(t, device=perm.device)[:, None] * k
+        return ops.moe_combine(d, top_k_weights, perm, inv[(base + order).reshape(-1)], t, k)
     d = d * top_k_weights.reshape(-1)[perm][:, None]
     contrib = torch.empty_like(d)
     contrib[perm] = d
     contrib = contrib.view(t, k, -1)
-    order = torch.argsort(top_k_index, dim=-1)  # each token's experts in ascending id: the eager add order
     contrib = torch.gather(contrib, 1, order[:, :, None].expand(-1, -1, contrib.shape[-1]))
     final = torch.zeros_like(hidden_states)
     for j in range(k):
@@ -124,29 +163,59 @@ EXPERT_STREAMS = int(os.environ.get("QZ_EXPERT_STREAMS", "4"))  # concurrent per
 _streams: Dict[torch.device, list] = {}
 
 
-def _per_expert_mm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, b) -> None:
-    """out[rows of e] = x[rows of e] @ w[e]^T for every routed expert e.  A routed expert's GEMM
-    is small (~2k rows: a few dozen output tiles on a 256-CU part), so the experts are spread
-    round-robin over EXPERT_STREAMS streams to run side by side; each GEMM is the same call on
-    the same operands whichever stream runs it, so the bits do not change."""
-    n = EXPERT_STREAMS if x.is_cuda else 1
-    if n <= 1:
-        for e in range(w.shape[0]):
-            if b[e + 1] > b[e]:
-                torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=out[b[e]:b[e + 1]])
-        return
-    main = torch.cuda.current_stream(x.device)
-    ss = _streams.get(x.device)
-    if ss is None or len(ss) != n:
-        ss = _streams[x.device] = [torch.cuda.Stream(x.device) for _ in range(n)]
-    for s in ss:
-        s.wait_stream(main)
+def _side_streams(dev: torch.device) -> list:
+    ss = _streams.get(dev)
+    if ss is None or len(ss) != EXPERT_STREAMS:
+        ss = _streams[dev] = [torch.cuda.Stream(dev) for _ in range(EXPERT_STREAMS)]
+    return ss
+
+
+def _expert_mms(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, b, n: int) -> list:
+    """The per-expert GEMM operands out[rows of e] = x[rows of e] @ w[e]^T of every routed expert,
+    dealt round-robin into ``n`` lists (one per stream).  Built once per plan: the views stay
+    valid because the plan's buffers and the expert parameters are rewritten in place."""
+    lists = [[] for _ in range(n)]
     for e in range(w.shape[0]):
         if b[e + 1] > b[e]:
-            with torch.cuda.stream(ss[e % n]):
-                torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=out[b[e]:b[e + 1]])
-    for s in ss:
-        main.wait_stream(s)
+            lists[e % n].append((x[b[e]:b[e + 1]], w[e].t(), out[b[e]:b[e + 1]]))
+    return lists
+
+
+def _run_mms(lists: list, dev: torch.device) -> None:
+    """Issue the GEMMs of ``_expert_mms``.  A routed expert's GEMM is small (~2k rows: a few dozen
+    output tiles on a 256-CU part), so the lists run on EXPERT_STREAMS streams side by side, each
+    list issued in one go from its stream; every GEMM is the same call on the same operands
+    whichever stream runs it, so the bits do not change."""
+    if len(lists) == 1:
+        for x, wt, o in lists[0]:
+            torch.mm(x, wt, out=o)
+        return
+    main = torch.cuda.current_stream(dev)
+    ss = _side_streams(dev)
+    for st in ss:
+        st.wait_stream(main)
+    for st, items in zip(ss, lists):
+        with torch.cuda.stream(st):
+            for x, wt, o in items:
+                torch.mm(x, wt, out=o)
+    for st in ss:
+        main.wait_stream(st)
+
+
+def _plan_buffers(m: nn.Module, hidden_states: torch.Tensor, p: Dict) -> Dict:
+    """The planned forward's intermediates, allocated once per plan, with every per-expert GEMM
+    operand view precomputed: a grid forward then costs the host one ``torch.mm`` per routed
+    expert GEMM and nothing else per expert."""
+    rows, dev, dt = p["tok"].numel(), hidden_states.device, hidden_states.dtype
+    n = EXPERT_STREAMS if hidden_states.is_cuda else 1
+    buf = {"xg": torch.empty(rows, hidden_states.shape[1], dtype=dt, device=dev),
+           "gu": torch.empty(rows, m.gate_up_proj.shape[1], dtype=dt, device=dev),
+           "h": torch.empty(rows, m.gate_up_proj.shape[1] // 2, dtype=dt, device=dev),
+           "d": torch.empty(rows, m.down_proj.shape[1], dtype=dt, device=dev)}
+    buf["mm1"] = _expert_mms(buf["xg"], m.gate_up_proj, buf["gu"], p["bounds"], n)
+    buf["mm2"] = _expert_mms(buf["h"], m.down_proj, buf["d"], p["bounds"], n)
+    buf["key"] = (dev, dt, tuple(hidden_states.shape))
+    return buf
 
 
 def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Tensor,
@@ -154,14 +223,16 @@ def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.
     """``fast_eager`` with the expert bounds on the host: one GEMM per routed expert over its
     rows of the expert-sorted tokens (the eager loop's per-expert GEMM shapes), no host sync."""
     t, k = top_k_index.shape
-    xg = hidden_states[p["tok"]]
-    b = p["bounds"]
-    gu = torch.empty(xg.shape[0], m.gate_up_proj.shape[1], dtype=xg.dtype, device=xg.device)
-    _per_expert_mm(xg, m.gate_up_proj, gu, b)
-    gate, up = gu.chunk(2, dim=-1)
-    h = m.act_fn(gate) * up
-    d = torch.empty(xg.shape[0], m.down_proj.shape[1], dtype=h.dtype, device=h.device)
-    _per_expert_mm(h, m.down_proj, d, b)
+    buf = p.get("buf")
+    if buf is None or buf["key"] != (hidden_states.device, hidden_states.dtype, tuple(hidden_states.shape)):
+        buf = p["buf"] = _plan_buffers(m, hidden_states, p)
+    xg, gu, h, d = buf["xg"], buf["gu"], buf["h"], buf["d"]
+    torch.index_select(hidden_states, 0, p["tok"], out=xg)
+    _run_mms(buf["mm1"], xg.device)
+    _act_mul(m, gu, out=h)
+    _run_mms(buf["mm2"], xg.device)
+    if _fused(d, top_k_weights, hidden_states):
+        return ops.moe_combine(d, top_k_weights, p["perm"], p["src"], t, k)
     d = d * top_k_weights.reshape(-1)[p["perm"]][:, None]
     contrib = d.index_select(0, p["src"]).view(t, k, -1)
     final = torch.zeros_like(hidden_states)

@@ -700,6 +700,50 @@ def scale_rows_(w: torch.Tensor, s: torch.Tensor, divide: bool = True) -> torch.
     return w
 
 
+def moe_combine(expert_out: torch.Tensor, top_k_weights: torch.Tensor, perm: torch.Tensor, src: torch.Tensor,
+                tokens: int, top_k: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qz_moe_combine: the eager experts loop's weighting and ascending-expert bf16 accumulation
+    in one pass.  ``expert_out`` [tokens * top_k, hidden] bf16 in expert-sorted order,
+    ``top_k_weights`` the router's [tokens, top_k] weights (bf16 or f32), ``perm`` the sort
+    permutation (sorted row -> flat (token, slot)), ``src`` the sorted row of each token's j-th
+    expert in ascending id ([tokens * top_k]).  Returns [tokens, hidden] bf16."""
+    _check_dev(expert_out, "expert_out")
+    if expert_out.dtype != torch.bfloat16 or top_k_weights.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"qz_moe_combine: bf16 expert outputs and bf16/f32 weights, got {expert_out.dtype}, "
+                        f"{top_k_weights.dtype}")
+    d = expert_out.contiguous()
+    w = top_k_weights.reshape(-1).contiguous()
+    perm = perm.to(torch.int64).contiguous()
+    src = src.to(torch.int64).contiguous()
+    if d.dim() != 2 or d.shape[0] != tokens * top_k or w.numel() != tokens * top_k or perm.numel() != d.shape[0] \
+            or src.numel() != d.shape[0]:
+        raise ValueError(f"qz_moe_combine: shapes {tuple(d.shape)}, weights {w.numel()}, perm {perm.numel()}, "
+                         f"src {src.numel()} for {tokens} tokens x top-{top_k}")
+    if out is None:
+        out = torch.empty(tokens, d.shape[1], dtype=torch.bfloat16, device=d.device)
+    rc = _lib.load().qz_moe_combine(_ptr(d), d.shape[0], d.shape[1], _ptr(w), int(w.dtype == torch.float32),
+                                    _ptr(perm), _ptr(src), tokens, top_k, _ptr(out), _stream())
+    _lib.check(rc, "qz_moe_combine")
+    return out
+
+
+def moe_silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qz_moe_silu_mul: ``silu(gate) * up`` for a [rows, 2 * inter] bf16 gate/up GEMM output
+    (gate = the first half of the columns) into a dense [rows, inter] bf16 tensor."""
+    _check_dev(gate_up, "gate_up")
+    if gate_up.dtype != torch.bfloat16 or gate_up.dim() != 2 or gate_up.stride(1) != 1 or gate_up.shape[1] % 2:
+        raise ValueError(f"qz_moe_silu_mul: a row-major [rows, 2 * inter] bf16 tensor, got {gate_up.dtype} "
+                         f"{tuple(gate_up.shape)} strides {gate_up.stride()}")
+    rows, inter = gate_up.shape[0], gate_up.shape[1] // 2
+    if out is None:
+        out = torch.empty(rows, inter, dtype=torch.bfloat16, device=gate_up.device)
+    if out.dtype != torch.bfloat16 or tuple(out.shape) != (rows, inter) or not out.is_contiguous():
+        raise ValueError(f"qz_moe_silu_mul: out must be a dense [{rows}, {inter}] bf16 tensor")
+    rc = _lib.load().qz_moe_silu_mul(_ptr(gate_up), rows, inter, gate_up.stride(0), _ptr(out), _stream())
+    _lib.check(rc, "qz_moe_silu_mul")
+    return out
+
+
 class PreparedQuantize:
     """A qz_quantize call with every argument marshalled once (bench / tight host loops):
     ``run(w)`` costs one ctypes call + one kernel launch.  Graph-capturable."""

@@ -2,10 +2,11 @@
 """Per-layer GPU busy fraction and kernel-time breakdown of an AWQ oneshot kernel trace
 (rocprofv3 --kernel-trace; a rocpd .db converted with rocpd2csv):
 
-  python scripts/e2e_breakdown.py <kernel_trace.csv> <layers> [plain-run log]
+  python scripts/e2e_breakdown.py <kernel_trace.csv> <layers> [plain-run log] [header]
 
 The oneshot region starts at the first embedding gather (layer-0 input capture); a layer starts
-at its first activation-statistics kernel (k_absmean_partial_v8)."""
+at its first activation-statistics kernel (k_absmean_1l, or k_absmean_partial on the two-launch
+path)."""
 import collections
 import csv
 import sys
@@ -34,17 +35,17 @@ def _category(k):
     return "torch elementwise / reduce / copy"
 
 
-def main(path, layers, plain=None):
-    print(f"# scripts/awq_e2e.py {layers} 16 2048 (Qwen3-4B dims, {layers} layers, 16 x 2048 calibration tokens, "
-          "int4 g128 AWQ, model resident on the device)")
-    print("# rocprofv3 --kernel-trace --stats (rocpd db -> rocpd2csv); scripts/e2e_breakdown.py")
+def main(path, layers, plain=None, header=None):
+    print("# " + (header or f"scripts/awq_e2e.py {layers} 16 2048 (Qwen3-4B dims, {layers} layers, 16 x 2048 "
+                  "calibration tokens, int4 g128 AWQ, model resident on the device)"))
+    print("# rocprofv3 --kernel-trace --output-format csv; scripts/e2e_breakdown.py")
     if plain:
         print("# plain run of the same command: " + open(plain).read().strip().splitlines()[-1])
     rows = list(csv.DictReader(open(path)))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     i0 = next(i for i, x in enumerate(iv) if "vectorized_gather_kernel" in x[2])
     sub = iv[i0:]
-    ab = [i for i, x in enumerate(sub) if "k_absmean_partial" in x[2]]
+    ab = [i for i, x in enumerate(sub) if "k_absmean_1l" in x[2] or "k_absmean_partial" in x[2]]
     per = len(ab) // layers
     marks = [ab[k] for k in range(0, per * layers, per)]
     span, busy = _busy(sub[:marks[0]])
@@ -74,4 +75,5 @@ def main(path, layers, plain=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3] if len(sys.argv) > 3 else None)
+    main(sys.argv[1], int(sys.argv[2]), sys.argv[3] if len(sys.argv) > 3 and sys.argv[3] else None,
+         sys.argv[4] if len(sys.argv) > 4 else None)

@@ -76,3 +76,97 @@ def test_fixed_routing_context_uses_plans():
         assert me._FIXED is None
         assert all(me.FastEagerExperts.planned_checked.values())
     assert torch.equal(got1, want) and torch.equal(got2, want)
+
+
+def _composed(d, w, perm, src, t, k):
+    """The composed PyTorch tail of fast_eager / planned_eager (the eager loop's arithmetic)."""
+    d = d * w.reshape(-1)[perm][:, None]
+    contrib = d.index_select(0, src).view(t, k, d.shape[1])
+    final = torch.zeros(t, d.shape[1], dtype=torch.bfloat16, device=d.device)
+    for j in range(k):
+        final = final + contrib[:, j].to(final.dtype)
+    return final
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hidden", [2048, 3072, 100, 8])
+@pytest.mark.parametrize("wdtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("tokens,k", [(300, 8), (257, 2), (1, 1), (0, 4)])
+def test_moe_combine_bit_identical(cuda, hidden, wdtype, tokens, k):
+    """qz_moe_combine == the composed weighting / reorder / k bf16 adds, bit for bit: wide and
+    narrow rows (16-B and scalar kernels), bf16 and f32 routing weights, signed zeros, infinities
+    and values whose bf16 sums round."""
+    from quantizers_amd import ops
+    g = torch.Generator().manual_seed(hidden * 31 + tokens * 7 + k)
+    n_exp = 16
+    idx = torch.stack([torch.randperm(n_exp, generator=g)[:k] for _ in range(tokens)]) if tokens else \
+        torch.empty(0, k, dtype=torch.int64)
+    w = torch.rand(tokens, k, generator=g).to(wdtype)
+    d = (torch.randn(tokens * k, hidden, generator=g) * 3).to(torch.bfloat16)
+    if d.numel():
+        d.view(-1)[::97] = -0.0
+        d.view(-1)[5::1013] = float("inf")
+        d.view(-1)[7::2039] = 65504.0
+    idx, w, d = idx.to(cuda), w.to(cuda), d.to(cuda)
+    flat = idx.reshape(-1)
+    _, perm = torch.sort(flat, stable=True)
+    order = torch.argsort(idx, dim=-1)
+    inv = torch.argsort(perm)
+    src = inv[(torch.arange(tokens, device=cuda)[:, None] * k + order).reshape(-1)]
+    got = ops.moe_combine(d, w, perm, src, tokens, k)
+    want = _composed(d, w, perm, src, tokens, k)
+    assert got.shape == want.shape == (tokens, hidden)
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    if tokens:  # unaligned expert outputs (a 1-element offset view) take the scalar kernel
+        big = torch.empty(d.numel() + 1, dtype=torch.bfloat16, device=cuda)
+        du = big[1:].view_as(d)
+        du.copy_(d)
+        got_u = ops.moe_combine(du, w, perm, src, tokens, k)
+        assert torch.equal(got_u.view(torch.int16), want.view(torch.int16))
+        with pytest.raises(ValueError):
+            ops.moe_combine(d[:-1], w, perm, src, tokens, k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("arch", ["qwen3_moe", "minimax"])
+def test_fused_forms_bit_identical_gpu(cuda, arch):
+    """On the GPU (qz_moe_combine tail): the grouped and the planned forms equal transformers'
+    eager fused-experts forward bit for bit."""
+    m = _models()[arch]().to(cuda)
+    ex = next(mod for mod in m.modules() if me.eager_forward(mod) is not None)
+    g = torch.Generator().manual_seed(11)
+    tokens, k = 300, 2
+    x = torch.randn(tokens, ex.gate_up_proj.shape[-1], generator=g).to(torch.bfloat16).to(cuda)
+    w, idx = torch.topk(torch.rand(tokens, ex.num_experts, generator=g).softmax(-1), k, dim=-1)
+    w, idx = (w / w.sum(-1, keepdim=True)).to(torch.bfloat16).to(cuda), idx.to(cuda)
+    with torch.no_grad():
+        want = me.eager_forward(ex)(ex, x, idx, w)
+        got = me.fast_eager(ex, x, idx, w)
+        planned = me.planned_eager(ex, x, idx, w, me._plan(ex, idx))
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    assert torch.equal(planned.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,inter", [(300, 768), (257, 1536), (5, 12), (0, 64)])
+def test_moe_silu_mul_bit_identical(cuda, rows, inter):
+    """qz_moe_silu_mul == F.silu(gate) * up over the gate/up GEMM output, bit for bit (16-B and
+    scalar kernels; large, tiny, signed-zero and infinite inputs).  The product path also
+    re-checks this on its first call (moe_eager._act_mul)."""
+    from quantizers_amd import ops
+    g = torch.Generator().manual_seed(rows + inter)
+    gu = (torch.randn(rows, 2 * inter, generator=g) * 4).to(torch.bfloat16)
+    if gu.numel():
+        gu.view(-1)[::53] = -0.0
+        gu.view(-1)[3::101] = float("inf")
+        gu.view(-1)[4::103] = -float("inf")
+        gu.view(-1)[6::107] = -90.0
+        gu.view(-1)[8::109] = 1e-38
+    gu = gu.to(cuda)
+    gate, up = gu.chunk(2, dim=-1)
+    want = torch.nn.functional.silu(gate) * up
+    got = ops.moe_silu_mul(gu)
+    assert got.shape == want.shape
+    nan = torch.isnan(want)
+    assert torch.equal(torch.isnan(got), nan)
+    assert torch.equal(got.view(torch.int16)[~nan], want.view(torch.int16)[~nan])

@@ -512,6 +512,7 @@ def test_moe_fast_eager_experts(cuda, monkeypatch, arch):
 
 
 @pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS", "BATCHED_LOSS", "moe_eager.PLANNED", "moe_eager.EXPERT_STREAMS",
+                                  "moe_eager.FUSED_COMBINE", "moe_eager.FUSED_ACT",
                                   "MULTI_LOSS"])
 def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
     """The expert-search speed knobs (experts-outer order; one GEMM for the per-expert inputs)
@@ -784,3 +785,35 @@ def test_concurrent_sample_calls_bit_identical(cuda, monkeypatch, arch):
             assert r.get("history") == r3[layer][smooth].get("history"), (layer, smooth)
     for n in p1:
         _eq(p1[n], p3[n], n)
+
+
+@pytest.mark.parametrize("arch", ["qwen3_moe", "minimax"])
+def test_grid_graph_replay_bit_identical(cuda, monkeypatch, arch):
+    """QZ_GRID_GRAPHS: the fixed-routing MoE-block grids replay their forward from one HIP graph
+    (checked against the eager forward on first use); the loss histories and smoothed
+    parameters equal the eager-forward run's bit for bit, and the replay path was the one taken."""
+    import quantizers_amd.awq as awq_mod
+    build = _qwen3_moe if arch == "qwen3_moe" else _minimax
+    recipe = os.path.join(ROOT, "configs", "recipes",
+                          "awq_w4a16_g32.yaml" if arch == "qwen3_moe" else "minimax_awq_mixedprec.yaml")
+    states = []
+    close = awq_mod._GraphedForward.close
+
+    def spy(self):
+        states.append(self.state)
+        close(self)
+    monkeypatch.setattr(awq_mod._GraphedForward, "close", spy)
+    out = {}
+    for on in (False, True):
+        monkeypatch.setattr(awq_mod, "GRID_GRAPHS", on)
+        m = build().to(cuda)
+        oneshot(m, recipe, dataset=_calib(n=5, vocab=256), max_seq_length=64)
+        out[on] = (m.awq_report, {n: p.detach().clone() for n, p in m.named_parameters()})
+    assert states and all(s is True for s in states), states
+    (r0, p0), (r1, p1) = out[False], out[True]
+    assert r0.keys() == r1.keys()
+    for layer in r0:
+        for smooth, r in r0[layer].items():
+            assert r.get("history") == r1[layer][smooth].get("history"), (layer, smooth)
+    for n in p0:
+        _eq(p0[n], p1[n], n)
