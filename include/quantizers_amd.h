@@ -74,7 +74,8 @@ enum {
   QZ_ERR_ASYM_FLOAT = -6,   /* "Asymmetric Quantization is not supported for FP4/FP8" */
   QZ_ERR_FORMAT = -7,       /* output format incompatible with args */
   QZ_ERR_WORKSPACE = -8,    /* workspace smaller than qz_quantize_workspace_size() */
-  QZ_ERR_ALIGN = -9         /* pointer/ld alignment violated where required */
+  QZ_ERR_ALIGN = -9,        /* pointer/ld alignment violated where required */
+  QZ_ERR_UNAVAILABLE = -10  /* a runtime dependency is not loaded / refused the call (qz_expert_gemms: hipBLASLt) */
 };
 
 const char* qz_strerror(int code);
@@ -345,6 +346,22 @@ int qz_moe_combine(const void* expert_out, int64_t rows, int64_t hidden, const v
  * composed ops on first use (the exp implementation is the device library's).
  */
 int qz_moe_silu_mul(const void* gate_up, int64_t rows, int64_t inter, int64_t ld, void* out,
+                    qz_stream_t stream);
+
+/*
+ * qz_expert_gemms -- the per-expert GEMMs of a fixed-routing MoE forward, issued in one call:
+ * for i < count, out[row0[i]:row1[i], :n] = x[row0[i]:row1[i], :k] @ w[expert[i]]^T, where
+ * w[e] is the [n, k] bf16 matrix at w + e * w_stride (row stride ldw), x / out bf16 with row
+ * strides ldx / ldo, all on `stream`.  Each GEMM is the hipBLASLt problem torch.mm(x[rows],
+ * w[e].t()) poses (f32 compute; the heuristic's first algorithm under a workspace limit of
+ * workspace_bytes), through the hipBLASLt already loaded in the process (PyTorch's); callers
+ * verify the bits against torch.mm before relying on them.  Replaces the eager experts loop's
+ * per-expert `nn.functional.linear` calls (transformers 4.57 per-expert MLPs, D15) in the
+ * fixed-routing forwards of an AWQ grid.  QZ_ERR_UNAVAILABLE without hipBLASLt.
+ */
+int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride, int64_t ldw, int64_t n,
+                    int64_t k, void* out, int64_t ldo, const int64_t* row0, const int64_t* row1,
+                    const int32_t* expert, int32_t count, void* workspace, size_t workspace_bytes,
                     qz_stream_t stream);
 
 #ifdef __cplusplus

@@ -1,0 +1,220 @@
+// qz_experts.hip -- the per-expert GEMMs of a fixed-routing MoE forward, issued from C (host code).
+//
+// An AWQ grid over an MoE block re-runs the block 21 times with the routing fixed (moe_eager.py,
+// planned form).  Every forward is two GEMMs per routed expert -- ~256 small hipBLASLt launches
+// -- and issued one `torch.mm` at a time from Python the host, not the GPU, sets the pace
+// (profiles/r03l_moe_breakdown.txt).  qz_expert_gemms issues a list of them in one call with
+// the Python GIL released: for each (row range, expert) it makes the call torch.mm(x[rows],
+// w[e].t(), out=out[rows]) makes -- the same hipBLASLt problem (column-major
+// D[n, m] = op_T(A = w[e]) * op_N(B = x[rows]), f32 compute, bf16 in/out, alpha 1, beta 0), the
+// heuristic's first algorithm under the same workspace limit -- so the same kernel and the same
+// bits; the caller verifies that against torch.mm on each plan's first forward before using it.
+//
+// hipBLASLt is not linked: the functions are looked up in the process (PyTorch's bundled
+// libhipblaslt, already loaded by torch), so there is exactly one copy of the library and its
+// kernel selection is torch's.  Without it loaded the call returns QZ_ERR_UNAVAILABLE
+// (QZ_EXPERT_GEMMS_DEBUG=1 prints which step refused).
+#include <dlfcn.h>
+#include <link.h>
+#include <hip/hip_runtime.h>
+#include <hipblaslt/hipblaslt.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+
+#include "../../include/quantizers_amd.h"
+
+namespace {
+
+struct LtApi {
+  decltype(&hipblasLtCreate) create = nullptr;
+  decltype(&hipblasLtMatmulDescCreate) desc_create = nullptr;
+  decltype(&hipblasLtMatmulDescSetAttribute) desc_set = nullptr;
+  decltype(&hipblasLtMatrixLayoutCreate) layout_create = nullptr;
+  decltype(&hipblasLtMatmulPreferenceCreate) pref_create = nullptr;
+  decltype(&hipblasLtMatmulPreferenceSetAttribute) pref_set = nullptr;
+  decltype(&hipblasLtMatmulPreferenceDestroy) pref_destroy = nullptr;
+  decltype(&hipblasLtMatmulAlgoGetHeuristic) heuristic = nullptr;
+  decltype(&hipblasLtMatmul) matmul = nullptr;
+  bool ok = false;
+};
+
+bool debug() {
+  static const bool d = [] {
+    const char* e = getenv("QZ_EXPERT_GEMMS_DEBUG");
+    return e && *e == '1';
+  }();
+  return d;
+}
+
+// The hipBLASLt already mapped into the process (PyTorch loads its bundled copy as a dependency
+// of libtorch_hip, RTLD_LOCAL: not visible through RTLD_DEFAULT).  Prefer torch's copy when
+// more than one is mapped.
+int find_lib(struct dl_phdr_info* info, size_t, void* data) {
+  std::string* best = (std::string*)data;
+  const char* path = info->dlpi_name;
+  if (!path || !strstr(path, "libhipblaslt.so")) return 0;
+  if (best->empty() || strstr(path, "/torch/lib/")) *best = path;
+  return 0;
+}
+
+void* lib_handle() {
+  std::string path;
+  dl_iterate_phdr(find_lib, &path);
+  void* h = path.empty() ? nullptr : dlopen(path.c_str(), RTLD_NOLOAD | RTLD_LAZY);
+  if (debug()) fprintf(stderr, "qz_expert_gemms: hipBLASLt %s (%p)\n", path.empty() ? "not mapped" : path.c_str(), h);
+  return h;
+}
+
+void* g_lib = nullptr;
+
+template <class F>
+void sym(F& f, const char* name) {
+  f = reinterpret_cast<F>(g_lib ? dlsym(g_lib, name) : dlsym(RTLD_DEFAULT, name));
+  if (!f && debug()) fprintf(stderr, "qz_expert_gemms: %s not found\n", name);
+}
+
+const LtApi& api() {
+  static LtApi a;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    g_lib = lib_handle();
+    sym(a.create, "hipblasLtCreate");
+    sym(a.desc_create, "hipblasLtMatmulDescCreate");
+    sym(a.desc_set, "hipblasLtMatmulDescSetAttribute");
+    sym(a.layout_create, "hipblasLtMatrixLayoutCreate");
+    sym(a.pref_create, "hipblasLtMatmulPreferenceCreate");
+    sym(a.pref_set, "hipblasLtMatmulPreferenceSetAttribute");
+    sym(a.pref_destroy, "hipblasLtMatmulPreferenceDestroy");
+    sym(a.heuristic, "hipblasLtMatmulAlgoGetHeuristic");
+    sym(a.matmul, "hipblasLtMatmul");
+    a.ok = a.create && a.desc_create && a.desc_set && a.layout_create && a.pref_create && a.pref_set &&
+           a.pref_destroy && a.heuristic && a.matmul;
+  });
+  return a;
+}
+
+// One GEMM problem: descriptors + the heuristic's algorithm, created once and kept (a few
+// hundred distinct row counts per model; descriptors are small host objects).
+struct Problem {
+  hipblasLtMatmulDesc_t desc = nullptr;
+  hipblasLtMatrixLayout_t a = nullptr, b = nullptr, c = nullptr;
+  hipblasLtMatmulAlgo_t algo{};
+};
+
+struct Key {
+  int dev;
+  int64_t m, n, k, lda, ldb, ldc;
+  uint64_t ws;
+  bool operator==(const Key& o) const {
+    return dev == o.dev && m == o.m && n == o.n && k == o.k && lda == o.lda && ldb == o.ldb && ldc == o.ldc &&
+           ws == o.ws;
+  }
+};
+struct KeyHash {
+  size_t operator()(const Key& x) const {
+    uint64_t h = 1469598103934665603ull;
+    for (uint64_t v : {(uint64_t)x.dev, (uint64_t)x.m, (uint64_t)x.n, (uint64_t)x.k, (uint64_t)x.lda, (uint64_t)x.ldb,
+                       (uint64_t)x.ldc, x.ws})
+      h = (h ^ v) * 1099511628211ull;
+    return (size_t)h;
+  }
+};
+
+// One mutex serialises every qz_expert_gemms call: the calls share one hipBLASLt handle per device
+// (whose matmul is not documented thread-safe) and the problem cache.  The product calls it from
+// one host thread (an AWQ grid); a second caller waits for the first call's launches.
+std::mutex g_mu;
+std::unordered_map<int, hipblasLtHandle_t> g_handles;
+std::unordered_map<Key, Problem, KeyHash> g_problems;
+
+// Looks up (or builds) the problem; the caller holds g_mu.  Returns 0 or a QZ_ERR_* / positive status.
+int problem(const LtApi& L, const Key& key, hipblasLtHandle_t* handle, const Problem** out) {
+  auto hit = g_handles.find(key.dev);
+  if (hit == g_handles.end()) {
+    hipblasLtHandle_t h = nullptr;
+    if (L.create(&h) != HIPBLAS_STATUS_SUCCESS) return QZ_ERR_UNAVAILABLE;
+    hit = g_handles.emplace(key.dev, h).first;
+  }
+  *handle = hit->second;
+  auto it = g_problems.find(key);
+  if (it != g_problems.end()) {
+    *out = &it->second;
+    return QZ_OK;
+  }
+  Problem p;
+  const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
+  if (L.desc_create(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F) != HIPBLAS_STATUS_SUCCESS ||
+      L.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)) != HIPBLAS_STATUS_SUCCESS ||
+      L.desc_set(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)) != HIPBLAS_STATUS_SUCCESS)
+    return QZ_ERR_UNAVAILABLE;
+  // column-major: A = w[e] seen as [k, n] (ld lda), op T; B = x[rows] seen as [k, m] (ld ldb);
+  // C = D = out[rows] seen as [n, m] (ld ldc)
+  if (L.layout_create(&p.a, HIP_R_16BF, key.k, key.n, key.lda) != HIPBLAS_STATUS_SUCCESS ||
+      L.layout_create(&p.b, HIP_R_16BF, key.k, key.m, key.ldb) != HIPBLAS_STATUS_SUCCESS ||
+      L.layout_create(&p.c, HIP_R_16BF, key.n, key.m, key.ldc) != HIPBLAS_STATUS_SUCCESS)
+    return QZ_ERR_UNAVAILABLE;
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (L.pref_create(&pref) != HIPBLAS_STATUS_SUCCESS) return QZ_ERR_UNAVAILABLE;
+  uint64_t ws = key.ws;
+  hipblasLtMatmulHeuristicResult_t res{};
+  int returned = 0;
+  hipblasStatus_t st = L.pref_set(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  if (st == HIPBLAS_STATUS_SUCCESS)
+    st = L.heuristic(*handle, p.desc, p.a, p.b, p.c, p.c, pref, 1, &res, &returned);
+  L.pref_destroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS || returned < 1 || res.state != HIPBLAS_STATUS_SUCCESS) {
+    if (debug())
+      fprintf(stderr, "qz_expert_gemms: heuristic status %d, %d results (m %ld n %ld k %ld)\n", (int)st, returned,
+              (long)key.m, (long)key.n, (long)key.k);
+    return QZ_ERR_UNAVAILABLE;
+  }
+  p.algo = res.algo;
+  *out = &g_problems.emplace(key, p).first->second;
+  return QZ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride, int64_t ldw, int64_t n, int64_t k,
+                    void* out, int64_t ldo, const int64_t* row0, const int64_t* row1, const int32_t* expert,
+                    int32_t count, void* workspace, size_t workspace_bytes, qz_stream_t stream) {
+  if (count < 0 || n <= 0 || k <= 0 || ldx < k || ldw < k || ldo < n) return QZ_ERR_SHAPE;
+  if (count == 0) return QZ_OK;
+  if (!x || !w || !out || !row0 || !row1 || !expert || (workspace_bytes && !workspace)) return QZ_ERR_NULL;
+  const LtApi& L = api();
+  if (!L.ok) return QZ_ERR_UNAVAILABLE;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return QZ_ERR_UNAVAILABLE;
+  std::lock_guard<std::mutex> lock(g_mu);
+  const float alpha = 1.0f, beta = 0.0f;
+  const uint16_t* xb = (const uint16_t*)x;
+  const uint16_t* wb = (const uint16_t*)w;
+  uint16_t* ob = (uint16_t*)out;
+  for (int32_t i = 0; i < count; ++i) {
+    const int64_t m = row1[i] - row0[i];
+    if (m < 0 || expert[i] < 0) return QZ_ERR_SHAPE;
+    if (m == 0) continue;
+    hipblasLtHandle_t h = nullptr;
+    const Problem* p = nullptr;
+    int rc = problem(L, Key{dev, m, n, k, ldw, ldx, ldo, (uint64_t)workspace_bytes}, &h, &p);
+    if (rc) return rc;
+    const hipblasStatus_t st =
+        L.matmul(h, p->desc, &alpha, wb + (int64_t)expert[i] * w_stride, p->a, xb + row0[i] * ldx, p->b, &beta,
+                 ob + row0[i] * ldo, p->c, ob + row0[i] * ldo, p->c, &p->algo, workspace, workspace_bytes,
+                 (hipStream_t)stream);
+    if (st != HIPBLAS_STATUS_SUCCESS) {
+      if (debug()) fprintf(stderr, "qz_expert_gemms: matmul status %d (m %ld)\n", (int)st, (long)m);
+      return QZ_ERR_UNAVAILABLE;
+    }
+  }
+  return QZ_OK;
+}
+
+}  // extern "C"

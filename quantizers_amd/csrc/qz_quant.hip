@@ -1380,6 +1380,7 @@ const char* qz_strerror(int code) {
     case QZ_ERR_FORMAT: return "output/scale format incompatible with the quantization args";
     case QZ_ERR_WORKSPACE: return "workspace too small";
     case QZ_ERR_ALIGN: return "alignment requirement violated";
+    case QZ_ERR_UNAVAILABLE: return "runtime dependency unavailable (hipBLASLt not loaded or refused the call)";
   }
   return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
 }

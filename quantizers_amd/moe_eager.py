@@ -177,7 +177,7 @@ def _expert_mms(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, b, n: int) 
     lists = [[] for _ in range(n)]
     for e in range(w.shape[0]):
         if b[e + 1] > b[e]:
-            lists[e % n].append((x[b[e]:b[e + 1]], w[e].t(), out[b[e]:b[e + 1]]))
+            lists[e % n].append((x[b[e]:b[e + 1]], w[e].t(), out[b[e]:b[e + 1]], b[e], b[e + 1], e))
     return lists
 
 
@@ -187,7 +187,7 @@ def _run_mms(lists: list, dev: torch.device) -> None:
     list issued in one go from its stream; every GEMM is the same call on the same operands
     whichever stream runs it, so the bits do not change."""
     if len(lists) == 1:
-        for x, wt, o in lists[0]:
+        for x, wt, o, *_ in lists[0]:
             torch.mm(x, wt, out=o)
         return
     main = torch.cuda.current_stream(dev)
@@ -196,41 +196,152 @@ def _run_mms(lists: list, dev: torch.device) -> None:
         st.wait_stream(main)
     for st, items in zip(ss, lists):
         with torch.cuda.stream(st):
-            for x, wt, o in items:
+            for x, wt, o, *_ in items:
                 torch.mm(x, wt, out=o)
     for st in ss:
         main.wait_stream(st)
 
 
-def _plan_buffers(m: nn.Module, hidden_states: torch.Tensor, p: Dict) -> Dict:
-    """The planned forward's intermediates, allocated once per plan, with every per-expert GEMM
-    operand view precomputed: a grid forward then costs the host one ``torch.mm`` per routed
-    expert GEMM and nothing else per expert."""
+DIRECT_GEMMS = os.environ.get("QZ_DIRECT_EXPERT_GEMMS", "1") == "1"  # A/B knob: qz_expert_gemms for the planned GEMMs
+# hipBLASLt workspace limit of the direct GEMMs: torch's (HIPBLASLT_WORKSPACE_SIZE / CUBLASLT_WORKSPACE_SIZE
+# in KiB), else its ROCm default; the algorithm choice depends on it, and each plan verifies the bits
+_WS_BYTES = int(os.environ.get("HIPBLASLT_WORKSPACE_SIZE", os.environ.get("CUBLASLT_WORKSPACE_SIZE", 76 * 1024))) * 1024
+_ws: Dict[int, torch.Tensor] = {}  # stream handle -> its hipBLASLt workspace
+
+
+def _direct_spec(bounds, n: int) -> list:
+    """Per stream: the (first row, end row, expert) arrays of the routed experts' GEMMs for
+    qz_expert_gemms, experts dealt round-robin over ``n`` streams as in ``_expert_mms``."""
+    import numpy as np
+    b = np.asarray(bounds, dtype=np.int64)
+    es = np.nonzero(b[1:] > b[:-1])[0]
+    spec = []
+    for st in range(n):
+        sel = es[es % n == st]
+        spec.append((np.ascontiguousarray(b[sel]), np.ascontiguousarray(b[sel + 1]), sel.astype(np.int32)))
+    return spec
+
+
+def _run_direct(spec: list, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
+    """The GEMMs of ``_expert_mms`` through qz_expert_gemms: one C call per stream, GIL released."""
+    from . import _lib
+    lib, dev = _lib.load(), x.device
+    main = torch.cuda.current_stream(dev)
+    ss = _side_streams(dev) if len(spec) > 1 else [main]
+    for st in ss:
+        if st is not main:
+            st.wait_stream(main)
+    for st, (r0, r1, ex) in zip(ss, spec):
+        if not len(r0):
+            continue
+        wsb = _ws.get(st.cuda_stream)  # one hipBLASLt workspace per stream (kernels on a stream serialise)
+        if wsb is None:
+            wsb = _ws[st.cuda_stream] = torch.empty(_WS_BYTES, dtype=torch.uint8, device=dev)
+        rc = lib.qz_expert_gemms(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), w.stride(1), w.shape[1],
+                                 w.shape[2], out.data_ptr(), out.stride(0), r0.ctypes.data, r1.ctypes.data,
+                                 ex.ctypes.data, len(r0), wsb.data_ptr(), _WS_BYTES, st.cuda_stream)
+        _lib.check(rc, "qz_expert_gemms")
+    for st in ss:
+        if st is not main:
+            main.wait_stream(st)
+
+
+def _plan_buffers(m: nn.Module, hidden_states: torch.Tensor, p: Dict, streams: int) -> Dict:
+    """The planned forward's intermediates, allocated once per plan.  The per-expert GEMMs run
+    either as one ``torch.mm`` per routed expert on precomputed operand views (built on first
+    use) or, on the GPU, as one qz_expert_gemms call per stream (verified against torch.mm for
+    every GEMM problem it has not run before)."""
     rows, dev, dt = p["tok"].numel(), hidden_states.device, hidden_states.dtype
-    n = EXPERT_STREAMS if hidden_states.is_cuda else 1
+    n = streams if hidden_states.is_cuda else 1
     buf = {"xg": torch.empty(rows, hidden_states.shape[1], dtype=dt, device=dev),
            "gu": torch.empty(rows, m.gate_up_proj.shape[1], dtype=dt, device=dev),
            "h": torch.empty(rows, m.gate_up_proj.shape[1] // 2, dtype=dt, device=dev),
-           "d": torch.empty(rows, m.down_proj.shape[1], dtype=dt, device=dev)}
-    buf["mm1"] = _expert_mms(buf["xg"], m.gate_up_proj, buf["gu"], p["bounds"], n)
-    buf["mm2"] = _expert_mms(buf["h"], m.down_proj, buf["d"], p["bounds"], n)
-    buf["key"] = (dev, dt, tuple(hidden_states.shape))
+           "d": torch.empty(rows, m.down_proj.shape[1], dtype=dt, device=dev), "n": n, "bounds": p["bounds"]}
+    buf["w1"], buf["w2"] = m.gate_up_proj, m.down_proj
+    direct = (DIRECT_GEMMS and hidden_states.is_cuda and dt == torch.bfloat16
+              and m.gate_up_proj.dtype == dt and m.down_proj.dtype == dt
+              and all(t.stride(-1) == 1 for t in (m.gate_up_proj, m.down_proj)))
+    buf["direct"] = None if direct else False  # None: to be verified on the first forward
+    if direct:
+        buf["spec1"] = buf["spec2"] = _direct_spec(p["bounds"], n)
+    buf["key"] = (dev, dt, tuple(hidden_states.shape), n)
     return buf
 
 
+def _torch_mms(buf: Dict, which: int) -> None:
+    lists = buf.get(f"mm{which}")
+    if lists is None:
+        x, w, out = (buf["xg"], buf["w1"], buf["gu"]) if which == 1 else (buf["h"], buf["w2"], buf["d"])
+        lists = buf[f"mm{which}"] = _expert_mms(x, w, out, buf["bounds"], buf["n"])
+    _run_mms(lists, buf["xg"].device)
+
+
+_DIRECT_LOGGED = [False]
+_VERIFIED: set = set()  # (device, m, n, k, strides) GEMM problems whose qz_expert_gemms bits equal torch.mm's
+
+
+def _problems(spec: list, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> set:
+    base = (x.device, w.shape[1], w.shape[2], x.stride(0), w.stride(1), out.stride(0))
+    return {base + (int(a1 - a0),) for r0, r1, _ in spec for a0, a1 in zip(r0, r1)}
+
+
+def _gemms(buf: Dict, which: int, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
+    """GEMM set ``which`` (1: gate/up, 2: down) of the plan.  A GEMM problem (shape, strides) the
+    direct path has not run before is verified first: the set runs both ways and the direct
+    path is kept only if its output equals torch.mm's bit for bit (a GEMM's bits depend only on
+    its problem and data, so one match per problem suffices)."""
+    spec = buf.get(f"spec{which}")
+    if buf["direct"] is None:
+        new = _problems(spec, x, w, out) - _VERIFIED
+        if not new:
+            buf[f"ok{which}"] = True
+        else:
+            _torch_mms(buf, which)
+            want = out.clone()
+            try:
+                _run_direct(spec, x, w, out)
+                ok = _bits_equal(out, want)
+            except RuntimeError as e:
+                log.info("MoE: qz_expert_gemms unavailable (%s); torch.mm per expert", e)
+                ok = False
+            if not ok:
+                out.copy_(want)
+                log.info("MoE: qz_expert_gemms differs from torch.mm at %s; torch.mm per expert", tuple(out.shape))
+                buf["direct"] = False
+                return
+            _VERIFIED.update(new)
+            buf[f"ok{which}"] = True
+            if which == 2 and not _DIRECT_LOGGED[0]:
+                _DIRECT_LOGGED[0] = True
+                log.info("MoE: per-expert GEMMs through qz_expert_gemms (each new GEMM problem checked bit for "
+                         "bit against torch.mm first)")
+            if buf.get("ok1") and buf.get("ok2"):
+                buf["direct"] = True
+            return
+        if buf.get("ok1") and buf.get("ok2"):
+            buf["direct"] = True
+    if buf["direct"] is False:
+        _torch_mms(buf, which)
+        return
+    _run_direct(spec, x, w, out)
+
+
 def planned_eager(m: nn.Module, hidden_states: torch.Tensor, top_k_index: torch.Tensor,
-                  top_k_weights: torch.Tensor, p: Dict) -> torch.Tensor:
+                  top_k_weights: torch.Tensor, p: Dict, streams: Optional[int] = None) -> torch.Tensor:
     """``fast_eager`` with the expert bounds on the host: one GEMM per routed expert over its
-    rows of the expert-sorted tokens (the eager loop's per-expert GEMM shapes), no host sync."""
+    rows of the expert-sorted tokens (the eager loop's per-expert GEMM shapes), no host sync.
+    ``streams``: the per-expert GEMMs spread over that many streams (default EXPERT_STREAMS; 1 =
+    the caller's stream, for calls already running side by side on their own streams)."""
     t, k = top_k_index.shape
+    n = EXPERT_STREAMS if streams is None else streams
     buf = p.get("buf")
-    if buf is None or buf["key"] != (hidden_states.device, hidden_states.dtype, tuple(hidden_states.shape)):
-        buf = p["buf"] = _plan_buffers(m, hidden_states, p)
+    if buf is None or buf["key"] != (hidden_states.device, hidden_states.dtype, tuple(hidden_states.shape), n):
+        buf = p["buf"] = _plan_buffers(m, hidden_states, p, n)
     xg, gu, h, d = buf["xg"], buf["gu"], buf["h"], buf["d"]
     torch.index_select(hidden_states, 0, p["tok"], out=xg)
-    _run_mms(buf["mm1"], xg.device)
+    _gemms(buf, 1, xg, m.gate_up_proj, gu)
     _act_mul(m, gu, out=h)
-    _run_mms(buf["mm2"], xg.device)
+    _gemms(buf, 2, h, m.down_proj, d)
     if _fused(d, top_k_weights, hidden_states):
         return ops.moe_combine(d, top_k_weights, p["perm"], p["src"], t, k)
     d = d * top_k_weights.reshape(-1)[p["perm"]][:, None]

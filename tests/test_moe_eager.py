@@ -170,3 +170,38 @@ def test_moe_silu_mul_bit_identical(cuda, rows, inter):
     nan = torch.isnan(want)
     assert torch.equal(torch.isnan(got), nan)
     assert torch.equal(got.view(torch.int16)[~nan], want.view(torch.int16)[~nan])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(1536, 2048), (2048, 768), (96, 64)])
+def test_expert_gemms_bit_identical(cuda, n, k):
+    """qz_expert_gemms (hipBLASLt called from C, one call per stream) == torch.mm(x[rows],
+    w[e].t()) per expert, bit for bit: expert row counts from 0 to a few thousand, experts out of
+    order, one stream."""
+    import numpy as np
+    from quantizers_amd import _lib
+    import quantizers_amd.moe_eager as me_
+    g = torch.Generator().manual_seed(n + k)
+    E = 9
+    counts = [0, 1, 7, 64, 300, 2049, 17, 128, 5]
+    b = [0]
+    for c in counts:
+        b.append(b[-1] + c)
+    x = (torch.randn(b[-1], k, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+    w = (torch.randn(E, n, k, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+    want = torch.zeros(b[-1], n, dtype=torch.bfloat16, device=cuda)
+    for e in range(E):
+        if counts[e]:
+            torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=want[b[e]:b[e + 1]])
+    order = [4, 0, 8, 2, 6, 1, 3, 5, 7]
+    r0 = np.array([b[e] for e in order], dtype=np.int64)
+    r1 = np.array([b[e + 1] for e in order], dtype=np.int64)
+    ex = np.array(order, dtype=np.int32)
+    got = torch.full_like(want, float("nan"))
+    ws = torch.empty(me_._WS_BYTES, dtype=torch.uint8, device=cuda)
+    rc = _lib.load().qz_expert_gemms(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), w.stride(1), n, k,
+                                     got.data_ptr(), got.stride(0), r0.ctypes.data, r1.ctypes.data, ex.ctypes.data,
+                                     len(order), ws.data_ptr(), me_._WS_BYTES, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, _lib.load().qz_strerror(rc)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int16), want.view(torch.int16))

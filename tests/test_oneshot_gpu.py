@@ -512,7 +512,7 @@ def test_moe_fast_eager_experts(cuda, monkeypatch, arch):
 
 
 @pytest.mark.parametrize("knob", ["EXPERT_MAJOR", "CONCAT_EXPERT_INPUTS", "OVERLAP_LOSS", "BATCHED_LOSS", "moe_eager.PLANNED", "moe_eager.EXPERT_STREAMS",
-                                  "moe_eager.FUSED_COMBINE", "moe_eager.FUSED_ACT",
+                                  "moe_eager.FUSED_COMBINE", "moe_eager.FUSED_ACT", "moe_eager.DIRECT_GEMMS",
                                   "MULTI_LOSS"])
 def test_expert_search_knobs_bit_identical(cuda, monkeypatch, knob):
     """The expert-search speed knobs (experts-outer order; one GEMM for the per-expert inputs)
