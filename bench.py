@@ -330,7 +330,7 @@ def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream, n=40):
     return res
 
 
-def awq_oneshot_layers(dev, n_layers=2, n_seq=16, seq=2048):
+def awq_oneshot_layers(dev, n_layers=3, n_seq=16, seq=2048):
     """BASELINE.json configs[1] end to end on a truncated model: Qwen3-4B (public dims, random
     bf16 weights: no checkpoint offline) with ``n_layers`` decoder layers, the AWQ int4-g128
     recipe, ``n_seq`` x ``seq`` random calibration tokens, through ``quantizers_amd.oneshot``
@@ -353,11 +353,16 @@ def awq_oneshot_layers(dev, n_layers=2, n_seq=16, seq=2048):
     t = time.perf_counter() - t0
     rep = model.awq_report
     n_map = sum(len(v) for v in rep.values())
+    per_layer = list(model.awq_layer_seconds)
     del model
     torch.cuda.empty_cache()
+    steady = sum(per_layer[1:]) / max(len(per_layer) - 1, 1)
     return {"model": "Qwen3-4B dims, random bf16 weights", "layers": n_layers, "calibration_tokens": n_seq * seq,
-            "mappings": n_map, "s_total": t, "s_per_layer": t / n_layers,
-            "projected_36_layers_s": t / n_layers * 36, "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
+            "mappings": n_map, "s_total": t, "s_per_layer_logged": per_layer, "s_per_steady_layer": steady,
+            "projected_36_layers_s": t + (36 - n_layers) * steady,
+            "how": "wall clock of oneshot() on the truncated model (layer-0 input capture and first-call setup "
+                   "included once); projection = that + the remaining layers at the mean of layers 1..n-1",
+            "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
 
 
 def build_model(dev):

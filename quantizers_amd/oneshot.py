@@ -113,7 +113,10 @@ def _layer_out(o):
 
 @torch.no_grad()
 def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report,
-                    calibrate_all_experts: bool = True, stateful_observers: bool = False, residency=None):
+                    calibrate_all_experts: bool = True, stateful_observers: bool = False, residency=None,
+                    seconds: Optional[List[float]] = None):
+    """``seconds`` collects each layer's host wall time (as logged)."""
+    seconds = [] if seconds is None else seconds
     layers = decoder_layers(model)
     lname = next(n for n, m in model.named_modules() if m is layers)
     weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
@@ -156,7 +159,9 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
             residency.release(layer)
         if host is not None:
             _offload(layer, host)
-        log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), time.time() - t0)
+        dt = time.time() - t0
+        seconds.append(dt)
+        log.info("AWQ layer %d: %d mappings in %.2fs", i, len(rep), dt)
         if awq_mod.PHASE_TIMING:
             log.info("AWQ phases so far (s): %s", {k: round(v, 3) for k, v in awq_mod.PHASES.items()})
 
@@ -192,6 +197,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     if not schemes:
         raise ValueError("recipe targets no module of this model")
     report: Dict[str, Any] = {}
+    layer_seconds: List[float] = []
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}  # the residency plan reads it
     from . import residency as residency_mod
     res = None
@@ -222,7 +228,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         with eager_experts(model):
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
-                                stateful_observers, residency=res)
+                                stateful_observers, residency=res, seconds=layer_seconds)
     elif res is not None:  # RTN: no calibration pass, but each rank still needs its shards' tensors
         stager = []
 
@@ -237,6 +243,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     model.quantization_modifiers = modifiers
     model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml
     model.awq_report = report
+    model.awq_layer_seconds = layer_seconds  # per decoder layer (and AWQ modifier), as logged
     if output_dir is not None:
         from .compressor import save_compressed
         save_compressed(model, output_dir)
