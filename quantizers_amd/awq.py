@@ -906,7 +906,15 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         return _grid(r, groups, run, x_mean, w_mean, grid_shard)
 
     def _grid(r, groups, run, x_mean, w_mean, grid_shard):
-        """Steps 3-4 of ``search``: the 20-point grid and its argmin."""
+        """Steps 3-4 of ``search``: the 20-point grid and its argmin.  Balance layers all inside
+        fused experts: the router and the cached inputs are unchanged by the grid, so the
+        experts' routing is fixed across its forwards (moe_eager.fixed_routing) -- the reference
+        forward included, which takes the planned form too."""
+        fixed = r.parent_kind == "module" and all(b.index is not None for b in r.balance)
+        with moe_eager.fixed_routing() if fixed else contextlib.nullcontext():
+            return _grid_fixed(r, groups, run, x_mean, w_mean, grid_shard, fixed)
+
+    def _grid_fixed(r, groups, run, x_mean, w_mean, grid_shard, fixed):
         ref_out = run()
         # 3. grid search: losses stay on the device.  Under torch.distributed (and outside a
         # sharded batch of mappings) the ratios are split over the ranks (SURVEY §8e): rank r
@@ -922,27 +930,22 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         if any(o is not None for o in obs):
             world, rank = 1, 0  # the observer memory runs through the grid in order: no ratio split
         losses = torch.zeros(n_grid, dtype=torch.float64, device=x_mean.device)
-        # balance layers all inside fused experts: the router and the cached inputs are unchanged
-        # by the grid, so the experts' routing is fixed across its forwards (moe_eager.fixed_routing)
-        fixed = r.parent_kind == "module" and all(b.index is not None for b in r.balance)
-        routing = moe_eager.fixed_routing() if fixed else contextlib.nullcontext()
         graphed = None
         if fixed and GRID_GRAPHS and x_mean.is_cuda:
             run = graphed = _GraphedForward(run, r.smooth_name)
-        with routing:
-            for i in range(rank, n_grid, world):
-                ratio = i / n_grid
-                ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
-                for g, w0, t, o in zip(groups, orig, tmp, obs):
-                    if o is not None:
-                        _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
-                        _view(g).copy_(t)
-                    elif len(g) == 1:
-                        ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
-                    else:
-                        ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
-                        _view(g).copy_(t)
-                losses[i] = _sq_err(ref_out, run())
+        for i in range(rank, n_grid, world):
+            ratio = i / n_grid
+            ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
+            for g, w0, t, o in zip(groups, orig, tmp, obs):
+                if o is not None:
+                    _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
+                    _view(g).copy_(t)
+                elif len(g) == 1:
+                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=g[0].weight)
+                else:
+                    ops.fake_quantize(w0, quantized[g[0].name], col_scales=scales, out=t)
+                    _view(g).copy_(t)
+            losses[i] = _sq_err(ref_out, run())
         if graphed is not None:
             graphed.close()
         for g, w0 in zip(groups, orig):
