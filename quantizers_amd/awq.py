@@ -385,21 +385,19 @@ class _ExpertInputs:
 
     def hidden(self, i: int, e: int) -> torch.Tensor:
         """act(x W_gate^T) * (x W_up^T) for expert e: the input of its down projection."""
-        gate, up = nn.functional.linear(self.tokens(i, e), self.gate_up0[e]).chunk(2, dim=-1)
-        return self.module.act_fn(gate) * up
+        return moe_eager._act_mul(self.module, nn.functional.linear(self.tokens(i, e), self.gate_up0[e]))
 
     def hidden_cat(self, e: int) -> torch.Tensor:
         """``cat([hidden(i, e) for every batch i])`` as ONE GEMM over the concatenated tokens:
         hipBLASLt gives every row the same bits either way at these shapes
-        (``scripts/concat_probe.py``), and a 128-expert layer issues 128 GEMMs instead of 2,048."""
+        (``profiles/r02ao_concat_probe.log``), and a 128-expert layer issues 128 GEMMs instead of 2,048."""
         if self.calibrate_all or any(t is None for t in self.topk):
             if self._xcat is None:
                 self._xcat = torch.cat(self.x) if len(self.x) > 1 else self.x[0]
             x = self._xcat
         else:
             x = torch.cat([self.tokens(i, e) for i in range(len(self.x))])
-        gate, up = nn.functional.linear(x, self.gate_up0[e]).chunk(2, dim=-1)
-        return self.module.act_fn(gate) * up
+        return moe_eager._act_mul(self.module, nn.functional.linear(x, self.gate_up0[e]))
 
 
 CONCAT_EXPERT_INPUTS = os.environ.get("QZ_CONCAT_EXPERT_INPUTS", "1") == "1"
@@ -900,8 +898,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
                 def run(x=xin, mod=mod, e=e):
                     outs = []
                     for t in x:
-                        gate, up = nn.functional.linear(t, mod.gate_up_proj[e]).chunk(2, dim=-1)
-                        outs.append(nn.functional.linear(mod.act_fn(gate) * up, mod.down_proj[e]))
+                        h = moe_eager._act_mul(mod, nn.functional.linear(t, mod.gate_up_proj[e]))
+                        outs.append(nn.functional.linear(h, mod.down_proj[e]))
                     return outs
         return _grid(r, groups, run, x_mean, w_mean, grid_shard)
 
