@@ -347,6 +347,14 @@ int qz_moe_combine(const void* expert_out, int64_t rows, int64_t hidden, const v
  */
 int qz_moe_silu_mul(const void* gate_up, int64_t rows, int64_t inter, int64_t ld, void* out,
                     qz_stream_t stream);
+/*
+ * qz_silu_mul -- the same for separate gate and up projections (a dense MLP, e.g. transformers
+ * 4.57 modeling_qwen3.Qwen3MLP.forward's `self.act_fn(self.gate_proj(x)) * self.up_proj(x)`):
+ * out[r, c] = bf16(bf16(silu(gate[r, c])) * up[r, c]), gate / up bf16 [rows, inter] with row
+ * strides ld_gate / ld_up, out dense [rows, inter] bf16.
+ */
+int qz_silu_mul(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up, int64_t rows, int64_t inter,
+                void* out, qz_stream_t stream);
 
 /*
  * qz_expert_gemms -- the per-expert GEMMs of a fixed-routing MoE forward, issued in one call:

@@ -7,8 +7,9 @@
 // +0 accumulator.  Composed from PyTorch ops that tail is a weighting pass, a row gather and k
 // strided adds over [tokens, hidden] -- ~7 passes over the expert outputs.  qz_moe_combine does
 // it in one: per token, read its k expert-sorted output rows in ascending expert order, weight
-// and add in registers with the same roundings, write the token row once.  qz_moe_silu_mul fuses
-// the `act_fn(gate) * up` between the two expert GEMMs (two strided passes) into one.
+// and add in registers with the same roundings, write the token row once.  qz_silu_mul /
+// qz_moe_silu_mul fuse the `act_fn(gate) * up` between the gate/up and down projections (two
+// passes) into one, for dense MLPs and experts alike.
 #include <hip/hip_runtime.h>
 
 #include "qz_device.h"
@@ -84,18 +85,20 @@ __global__ __launch_bounds__(CB_THREADS) void k_moe_combine_v1(const uint16_t* _
   out[t * H + c] = f2bf(acc);
 }
 
-// act(gate) * up over the [rows, 2 * inter] gate/up GEMM output (gate = the first inter columns):
-// torch's silu kernel (x / (1 + exp(-x)) in f32, rounded to bf16) then the bf16 product.
+// silu(gate) * up: torch's silu kernel (x / (1 + exp(-x)) in f32, rounded to bf16) then the bf16
+// product; gate and up are [rows, inter] with their own row strides (the two halves of one fused
+// gate/up GEMM output, or two separate projections), out is dense [rows, inter].
 __device__ __forceinline__ float silu_bf16(float x) { return bfr(x / (1.0f + expf(-x))); }
 
-__global__ __launch_bounds__(256) void k_silu_mul_v8(const uint16_t* __restrict__ gu, int64_t rows, int64_t inter,
-                                                     int64_t ld, uint16_t* __restrict__ h) {
+__global__ __launch_bounds__(256) void k_silu_mul_v8(const uint16_t* __restrict__ gate, int64_t ldg,
+                                                     const uint16_t* __restrict__ up, int64_t ldu, int64_t rows,
+                                                     int64_t inter, uint16_t* __restrict__ h) {
   const int64_t per_row = inter / 8;
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * per_row) return;
   const int64_t r = i / per_row, c = (i % per_row) * 8;
-  const uint4 g = *(const uint4*)(gu + r * ld + c);
-  const uint4 u = *(const uint4*)(gu + r * ld + inter + c);
+  const uint4 g = *(const uint4*)(gate + r * ldg + c);
+  const uint4 u = *(const uint4*)(up + r * ldu + c);
   const uint32_t ga[4] = {g.x, g.y, g.z, g.w}, ua[4] = {u.x, u.y, u.z, u.w};
   uint32_t o[4];
 #pragma unroll
@@ -107,12 +110,13 @@ __global__ __launch_bounds__(256) void k_silu_mul_v8(const uint16_t* __restrict_
   *(uint4*)(h + r * inter + c) = make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-__global__ __launch_bounds__(256) void k_silu_mul_v1(const uint16_t* __restrict__ gu, int64_t rows, int64_t inter,
-                                                     int64_t ld, uint16_t* __restrict__ h) {
+__global__ __launch_bounds__(256) void k_silu_mul_v1(const uint16_t* __restrict__ gate, int64_t ldg,
+                                                     const uint16_t* __restrict__ up, int64_t ldu, int64_t rows,
+                                                     int64_t inter, uint16_t* __restrict__ h) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * inter) return;
   const int64_t r = i / inter, c = i % inter;
-  h[r * inter + c] = f2bf(silu_bf16(bf2f(gu[r * ld + c])) * bf2f(gu[r * ld + inter + c]));
+  h[r * inter + c] = f2bf(silu_bf16(bf2f(gate[r * ldg + c])) * bf2f(up[r * ldu + c]));
 }
 
 }  // namespace
@@ -146,21 +150,30 @@ int qz_moe_combine(const void* expert_out, int64_t rows, int64_t hidden, const v
   return launch_err();
 }
 
-int qz_moe_silu_mul(const void* gate_up, int64_t rows, int64_t inter, int64_t ld, void* out, qz_stream_t stream) {
-  if (rows < 0 || inter <= 0 || ld < 2 * inter) return QZ_ERR_SHAPE;
+int qz_silu_mul(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up, int64_t rows, int64_t inter,
+                void* out, qz_stream_t stream) {
+  if (rows < 0 || inter <= 0 || ld_gate < inter || ld_up < inter) return QZ_ERR_SHAPE;
   if (rows == 0) return QZ_OK;
-  if (!gate_up || !out) return QZ_ERR_NULL;
-  const bool v8 = inter % 8 == 0 && ld % 8 == 0 && aligned(gate_up, 16) && aligned(out, 16);
+  if (!gate || !up || !out) return QZ_ERR_NULL;
+  const bool v8 = inter % 8 == 0 && ld_gate % 8 == 0 && ld_up % 8 == 0 && aligned(gate, 16) && aligned(up, 16) &&
+                  aligned(out, 16);
   const int64_t n = v8 ? rows * (inter / 8) : rows * inter;
   if (cdiv(n, 256) > 0x7fffffffLL) return QZ_ERR_SHAPE;
   const dim3 grid((unsigned)cdiv(n, 256)), block(256);
   if (v8)
-    hipLaunchKernelGGL(k_silu_mul_v8, grid, block, 0, (hipStream_t)stream, (const uint16_t*)gate_up, rows, inter, ld,
-                       (uint16_t*)out);
+    hipLaunchKernelGGL(k_silu_mul_v8, grid, block, 0, (hipStream_t)stream, (const uint16_t*)gate, ld_gate,
+                       (const uint16_t*)up, ld_up, rows, inter, (uint16_t*)out);
   else
-    hipLaunchKernelGGL(k_silu_mul_v1, grid, block, 0, (hipStream_t)stream, (const uint16_t*)gate_up, rows, inter, ld,
-                       (uint16_t*)out);
+    hipLaunchKernelGGL(k_silu_mul_v1, grid, block, 0, (hipStream_t)stream, (const uint16_t*)gate, ld_gate,
+                       (const uint16_t*)up, ld_up, rows, inter, (uint16_t*)out);
   return launch_err();
+}
+
+int qz_moe_silu_mul(const void* gate_up, int64_t rows, int64_t inter, int64_t ld, void* out, qz_stream_t stream) {
+  if (rows < 0 || inter <= 0 || ld < 2 * inter) return QZ_ERR_SHAPE;
+  if (rows == 0) return QZ_OK;
+  if (!gate_up) return QZ_ERR_NULL;
+  return qz_silu_mul(gate_up, ld, (const uint16_t*)gate_up + inter, ld, rows, inter, out, stream);
 }
 
 }  // extern "C"

@@ -744,6 +744,27 @@ def moe_silu_mul(gate_up: torch.Tensor, out: Optional[torch.Tensor] = None) -> t
     return out
 
 
+def silu_mul(gate: torch.Tensor, up: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qz_silu_mul: ``silu(gate) * up`` for two bf16 [rows, inter] tensors (row-major, any row
+    stride) into a dense [rows, inter] bf16 tensor (leading dims of the inputs are flattened)."""
+    _check_dev(gate, "gate")
+    if gate.dtype != torch.bfloat16 or up.dtype != torch.bfloat16 or gate.shape != up.shape:
+        raise ValueError(f"qz_silu_mul: two bf16 tensors of one shape, got {gate.dtype} {tuple(gate.shape)}, "
+                         f"{up.dtype} {tuple(up.shape)}")
+    shape = gate.shape
+    g2, u2 = gate.reshape(-1, shape[-1]), up.reshape(-1, shape[-1])
+    if g2.stride(1) != 1 or u2.stride(1) != 1:
+        raise ValueError("qz_silu_mul: rows must be contiguous")
+    if out is None:
+        out = torch.empty(shape, dtype=torch.bfloat16, device=gate.device)
+    if out.dtype != torch.bfloat16 or out.shape != shape or not out.is_contiguous():
+        raise ValueError(f"qz_silu_mul: out must be a dense {tuple(shape)} bf16 tensor")
+    rc = _lib.load().qz_silu_mul(_ptr(g2), g2.stride(0), _ptr(u2), u2.stride(0), g2.shape[0], g2.shape[1],
+                                 _ptr(out), _stream())
+    _lib.check(rc, "qz_silu_mul")
+    return out
+
+
 class PreparedQuantize:
     """A qz_quantize call with every argument marshalled once (bench / tight host loops):
     ``run(w)`` costs one ctypes call + one kernel launch.  Graph-capturable."""
