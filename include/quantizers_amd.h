@@ -372,6 +372,17 @@ int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride,
                     const int32_t* expert, int32_t count, void* workspace, size_t workspace_bytes,
                     qz_stream_t stream);
 
+/*
+ * qz_rmsnorm128 -- RMSNorm over rows of 128 bf16 (row stride ld, ld % 4 == 0, 8-B aligned) into a
+ * dense [rows, 128] bf16 out, in the model's own arithmetic: f32 squares summed in the order of
+ * PyTorch's reduce kernel for a 128-wide row (32 threads x 4, shuffle tree), times 1/128, + eps,
+ * correctly rounded rsqrt, bf16(x * r), bf16(weight * y) -- bit-identical to transformers 4.57
+ * modeling_qwen3.Qwen3RMSNorm.forward for the q / k head norms (head_dim 128)
+ * (profiles/r03t_rmsnorm_probe.log); callers still check it on first use.
+ */
+int qz_rmsnorm128(const void* x, int64_t rows, int64_t ld, const void* weight, float eps, void* out,
+                  qz_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,91 @@
+"""The models' 128-wide RMSNorms (Qwen3's q / k head norms) in one HIP pass during the AWQ pass.
+
+transformers' Qwen3RMSNorm.forward (the reference pins 4.57) runs ~8 PyTorch kernels with f32
+intermediates per call, and every attention forward of the AWQ grid calls it twice (q_norm,
+k_norm) over [tokens, heads, 128].  ``fused_rmsnorms`` gives every module whose class forward is
+that exact code (bytecode-equal to ``_reference_forward``) a forward that runs ``qz_rmsnorm128``
+(csrc/qz_norm.hip: PyTorch's summation order and roundings, established by
+scripts/rmsnorm_probe.py) for bf16 GPU inputs whose last dim is 128 -- compared bit for bit with
+the module's own forward on its first call per device, and not used again if they differ.
+Other widths (the 2560-wide layer norms) take the module's own forward."""
+from __future__ import annotations
+
+import contextlib
+import logging
+import os
+from typing import Dict
+
+import torch
+from torch import nn
+
+from . import ops
+from .moe_eager import _bits_equal
+
+log = logging.getLogger(__name__)
+
+FUSED_NORM = os.environ.get("QZ_FUSED_NORM", "1") == "1"  # A/B knob: qz_rmsnorm128 for 128-wide RMSNorms
+_OK: Dict[torch.device, bool] = {}  # qz_rmsnorm128 verified against the module's forward (per device)
+
+
+def _reference_forward(self, hidden_states: torch.Tensor) -> torch.Tensor:
+    input_dtype = hidden_states.dtype
+    hidden_states = hidden_states.to(torch.float32)
+    variance = hidden_states.pow(2).mean(-1, keepdim=True)
+    hidden_states = hidden_states * torch.rsqrt(variance + self.variance_epsilon)
+    return self.weight * hidden_states.to(input_dtype)
+
+
+def qualifies(m: nn.Module) -> bool:
+    fwd = type(m).forward
+    fwd = getattr(fwd, "__wrapped__", fwd)
+    code, ref = getattr(fwd, "__code__", None), _reference_forward.__code__
+    return (code is not None and code.co_code == ref.co_code and code.co_names == ref.co_names
+            and isinstance(getattr(m, "weight", None), torch.Tensor) and hasattr(m, "variance_epsilon"))
+
+
+class FusedRMSNorm:
+    """Instance-level forward for one qualifying RMSNorm (see the module docstring)."""
+
+    def __init__(self, module: nn.Module, own):
+        self.m, self.own = module, own
+
+    def forward(self, hidden_states: torch.Tensor) -> torch.Tensor:
+        m, x = self.m, hidden_states
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and m.weight.dtype == torch.bfloat16 and x.shape[-1] == 128
+                and m.weight.numel() == 128 and x.numel() and x.stride(-1) == 1 and x.data_ptr() % 8 == 0
+                and all(s % 4 == 0 for s in x.stride()[:-1])):
+            return self.own(x)
+        ok = _OK.get(x.device)
+        if ok is None:
+            want = self.own(x)
+            try:
+                ok = _bits_equal(ops.rmsnorm128(x, m.weight, m.variance_epsilon), want)
+            except (RuntimeError, ValueError) as e:
+                log.info("norm: qz_rmsnorm128 unavailable (%s)", e)
+                ok = False
+            _OK[x.device] = ok
+            if not ok:
+                log.info("norm: qz_rmsnorm128 differs from %s.forward on %s; the module's own forward kept",
+                         type(m).__name__, x.device)
+            return want
+        if not ok:
+            return self.own(x)
+        return ops.rmsnorm128(x, m.weight, m.variance_epsilon)
+
+
+@contextlib.contextmanager
+def fused_rmsnorms(model: nn.Module):
+    """Every qualifying RMSNorm of ``model`` forwards through ``FusedRMSNorm`` inside the context;
+    the class forwards are restored after."""
+    patched = []
+    try:
+        if FUSED_NORM:
+            for mod in model.modules():
+                if "forward" not in mod.__dict__ and qualifies(mod):
+                    mod.forward = FusedRMSNorm(mod, mod.forward).forward  # bound class forward kept as "own"
+                    patched.append(mod)
+        yield len(patched)
+    finally:
+        for mod in patched:
+            if "forward" in mod.__dict__:
+                del mod.forward

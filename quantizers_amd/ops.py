@@ -765,6 +765,24 @@ def silu_mul(gate: torch.Tensor, up: torch.Tensor, out: Optional[torch.Tensor] =
     return out
 
 
+def rmsnorm128(x: torch.Tensor, weight: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """qz_rmsnorm128: Qwen3RMSNorm's forward over the last dim (128) of a bf16 tensor whose rows
+    are contiguous (row stride a multiple of 4 elements, 8-B aligned), with a bf16 weight."""
+    _check_dev(x, "x")
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16 or x.shape[-1] != 128 or weight.numel() != 128:
+        raise ValueError(f"qz_rmsnorm128: bf16 [..., 128] input and bf16 [128] weight, got {x.dtype} "
+                         f"{tuple(x.shape)}, {weight.dtype} {tuple(weight.shape)}")
+    x2 = x.reshape(-1, 128)
+    if x2.stride(1) != 1:
+        raise ValueError("qz_rmsnorm128: rows must be contiguous")
+    w = weight.contiguous()
+    if out is None:
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    rc = _lib.load().qz_rmsnorm128(_ptr(x2), x2.shape[0], x2.stride(0), _ptr(w), float(eps), _ptr(out), _stream())
+    _lib.check(rc, "qz_rmsnorm128")
+    return out
+
+
 class PreparedQuantize:
     """A qz_quantize call with every argument marshalled once (bench / tight host loops):
     ``run(w)`` costs one ctypes call + one kernel launch.  Graph-capturable."""
