@@ -383,6 +383,18 @@ int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride,
 int qz_rmsnorm128(const void* x, int64_t rows, int64_t ld, const void* weight, float eps, void* out,
                   qz_stream_t stream);
 
+/*
+ * qz_rotary128 -- rotary position embedding of 128-wide heads in the model's own arithmetic:
+ * out = bf16(bf16(x * cos) + bf16(rotate_half(x) * sin)), rotate_half(x) = cat(-x[64:], x[:64]).
+ * x / out: bf16 [B, H, T, 128] with element strides (xb, xh, xt) / (ob, oh, ot), the last dim
+ * contiguous; cos / sin: bf16 [B, T, 128] with strides (cb, ct), broadcast over H.  All strides
+ * multiples of 4, pointers 8-B aligned.  Replaces transformers 4.57
+ * modeling_qwen3.apply_rotary_pos_emb (its three elementwise kernels and the rotate_half cat).
+ */
+int qz_rotary128(const void* x, int64_t B, int64_t H, int64_t T, int64_t xb, int64_t xh, int64_t xt,
+                 const void* cos, const void* sin, int64_t cb, int64_t ct, void* out, int64_t ob, int64_t oh,
+                 int64_t ot, qz_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,7 @@ EXPORTS = (
     "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
     "qz_awq_sq_err_partials_multi", "qz_awq_stats_layout", "qz_moe_combine",
     "qz_moe_silu_mul", "qz_expert_gemms", "qz_silu_mul", "qz_rmsnorm128",
+    "qz_rotary128",
 )
 
 
@@ -96,6 +97,7 @@ def load() -> ctypes.CDLL:
         "qz_moe_silu_mul": ([P, I64, I64, I64, P, P], ctypes.c_int),
         "qz_silu_mul": ([P, I64, P, I64, I64, I64, P, P], ctypes.c_int),
         "qz_rmsnorm128": ([P, I64, I64, P, ctypes.c_float, P, P], ctypes.c_int),
+        "qz_rotary128": ([P, I64, I64, I64, I64, I64, I64, P, P, I64, I64, P, I64, I64, I64, P], ctypes.c_int),
         "qz_expert_gemms": ([P, I64, P, I64, I64, I64, I64, P, I64, P, P, P, I32, P, SZ, P], ctypes.c_int),
     }
     for name, (argtypes, restype) in sig.items():

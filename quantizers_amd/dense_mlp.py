@@ -22,6 +22,7 @@ from torch import nn
 
 from . import ops
 from .moe_eager import _bits_equal
+from .patching import same_code
 
 log = logging.getLogger(__name__)
 
@@ -35,10 +36,7 @@ def _reference_forward(self, x):
 
 
 def qualifies(m: nn.Module) -> bool:
-    fwd = type(m).forward
-    fwd = getattr(fwd, "__wrapped__", fwd)
-    code, ref = getattr(fwd, "__code__", None), _reference_forward.__code__
-    return (code is not None and code.co_code == ref.co_code and code.co_names == ref.co_names
+    return (same_code(type(m).forward, _reference_forward)
             and all(isinstance(getattr(m, n, None), nn.Linear) for n in ("gate_proj", "up_proj", "down_proj"))
             and type(getattr(m, "act_fn", None)).__name__ in ("SiLUActivation", "SiLU")
             and not getattr(m.act_fn, "inplace", False))

@@ -20,6 +20,7 @@ from torch import nn
 
 from . import ops
 from .moe_eager import _bits_equal
+from .patching import same_code
 
 log = logging.getLogger(__name__)
 
@@ -36,10 +37,7 @@ def _reference_forward(self, hidden_states: torch.Tensor) -> torch.Tensor:
 
 
 def qualifies(m: nn.Module) -> bool:
-    fwd = type(m).forward
-    fwd = getattr(fwd, "__wrapped__", fwd)
-    code, ref = getattr(fwd, "__code__", None), _reference_forward.__code__
-    return (code is not None and code.co_code == ref.co_code and code.co_names == ref.co_names
+    return (same_code(type(m).forward, _reference_forward)
             and isinstance(getattr(m, "weight", None), torch.Tensor) and hasattr(m, "variance_epsilon"))
 
 

@@ -25,6 +25,7 @@ from torch import nn
 from . import awq as awq_mod
 from .dense_mlp import fused_mlps
 from .dense_norm import fused_rmsnorms
+from .rotary import fused_rotary
 from .moe_eager import eager_experts
 from .model import checkpoint_name, decoder_layers, iter_linears, model_type
 from .quantization import QuantizationScheme
@@ -227,7 +228,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         if res is not None:
             res.materialise_outside(model, decoder_layers(model))
         # MoE experts in the reference's (transformers 4.57) eager arithmetic, at grouped speed (D15)
-        with eager_experts(model), fused_mlps(model), fused_rmsnorms(model):
+        with eager_experts(model), fused_mlps(model), fused_rmsnorms(model), fused_rotary(model):
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
                                 stateful_observers, residency=res, seconds=layer_seconds)

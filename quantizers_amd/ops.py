@@ -783,6 +783,27 @@ def rmsnorm128(x: torch.Tensor, weight: torch.Tensor, eps: float, out: Optional[
     return out
 
 
+def rotary128(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """qz_rotary128: ``x * cos + rotate_half(x) * sin`` (apply_rotary_pos_emb with unsqueeze_dim=1)
+    for a bf16 [B, H, T, 128] ``x`` at any strides and bf16 [B, T, 128] ``cos`` / ``sin``; the
+    output has ``x``'s memory layout (as PyTorch's elementwise result would)."""
+    _check_dev(x, "x")
+    if (x.dim() != 4 or x.shape[-1] != 128 or cos.shape != sin.shape or cos.dim() != 3
+            or cos.shape[0] not in (1, x.shape[0]) or cos.shape[1] != x.shape[2] or cos.shape[2] != 128
+            or any(t.dtype != torch.bfloat16 for t in (x, cos, sin)) or x.stride(-1) != 1
+            or cos.stride() != sin.stride() or cos.stride(-1) != 1):
+        raise ValueError(f"qz_rotary128: bf16 x [B, H, T, 128] and cos / sin [B, T, 128], got {tuple(x.shape)} "
+                         f"{x.dtype}, {tuple(cos.shape)} {cos.dtype}")
+    out = torch.empty_like(x)
+    B, H, T, _ = x.shape
+    cb = cos.stride(0) if cos.shape[0] == B and B > 1 else 0
+    rc = _lib.load().qz_rotary128(_ptr(x), B, H, T, x.stride(0), x.stride(1), x.stride(2), _ptr(cos), _ptr(sin),
+                                  cb, cos.stride(1), _ptr(out), out.stride(0), out.stride(1), out.stride(2),
+                                  _stream())
+    _lib.check(rc, "qz_rotary128")
+    return out
+
+
 class PreparedQuantize:
     """A qz_quantize call with every argument marshalled once (bench / tight host loops):
     ``run(w)`` costs one ctypes call + one kernel launch.  Graph-capturable."""
