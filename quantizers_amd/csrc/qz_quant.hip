@@ -754,11 +754,24 @@ __device__ __forceinline__ void fq_load_tile(uint4 (&v)[U], const uint4* src, in
   }
 }
 
+#ifndef QZ_FQ_ST_AUX
+#define QZ_FQ_ST_AUX 16  // cache policy of the buffer stores: sc1 (gfx950 CPol SC1 = 16)
+#endif
+#ifndef QZ_FQ_BUF
+#define QZ_FQ_BUF 1  // 1: one-tile waves load / store through wave-uniform buffer descriptors (A/B knob)
+#endif
+// wave-uniform 64-bit value, provably so to the compiler (SGPRs)
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32);
+}
+
 template <int LOGL, int KIND, bool SYM, bool NT>
 __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   constexpr int U = FQ_ROWS;
   const int lane = threadIdx.x & (WAVE - 1);
-  const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + (threadIdx.x >> 6);  // a block of FQ_TILES tiles
+  // a block of FQ_TILES tiles (wave index through readfirstlane: wave-uniform to the compiler)
+  const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (rblk * U * FQ_TILES >= rows) return;
   const int64_t b = blockIdx.z;
   const int64_t upr = A.units_per_row;
@@ -767,7 +780,31 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   const int64_t cuc = col_ok ? cu : upr - 1;
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
   uint4 v[U];
-  fq_load_tile<NT, U>(v, src, rblk * U * FQ_TILES, rows, upr, cuc);
+  // one tile per wave: the tile's rows through one source and one destination descriptor
+  // (wave-uniform bases, 32-bit lane / row offsets: no per-unit 64-bit address arithmetic); rows
+  // past the slice re-read its last row and are not stored, nor are lanes past the last column
+  constexpr bool BUF = QZ_FQ_BUF && FQ_TILES == 1 && !NT;
+  uint32_t voff = 0, roff[U];
+  __amdgpu_buffer_rsrc_t rs_dst;
+  int nrow_b = 0;
+  if constexpr (BUF) {
+    const int64_t r0 = rblk * U;
+    nrow_b = (int)min<int64_t>(U, rows - r0);
+    const uint32_t rowb = (uint32_t)upr * 16u;
+    voff = (uint32_t)cuc * 16u;
+#pragma unroll
+    for (int u = 0; u < U; ++u) roff[u] = __builtin_amdgcn_readfirstlane((uint32_t)min(u, nrow_b - 1) * rowb);
+    const auto rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)uni64((uint64_t)(src + r0 * upr)), 0, 0x7fffffff,
+                                                          0x00020000);
+    rs_dst = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)uni64((uint64_t)(reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + r0 * upr)), 0, 0x7fffffff,
+        0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], 0));
+  } else {
+    fq_load_tile<NT, U>(v, src, rblk * U * FQ_TILES, rows, upr, cuc);
+  }
   // this lane's 8 column scales, their reciprocals, and whether rcp is accurate for all 8
   const float* csp = A.col_scales + b * A.cs_ld_batch + cuc * 8;
   const float4 c_lo = *reinterpret_cast<const float4*>(csp);
@@ -782,6 +819,15 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
              (fabsf(cs[k].y) <= 0x1.0p+100f);
   }
   const QP p = A.p;
+  if constexpr (BUF) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
+      if (col_ok && u < nrow_b)  // sc1 (write-through) as st_out
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs_dst, voff, roff[u], QZ_FQ_ST_AUX);
+    }
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < FQ_TILES; ++t) {
     const int64_t r0 = (rblk * FQ_TILES + t) * U;
