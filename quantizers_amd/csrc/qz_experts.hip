@@ -25,6 +25,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
 
 #include "../../include/quantizers_amd.h"
 
@@ -215,6 +216,63 @@ int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride,
     }
   }
   return QZ_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// GEMM algorithm probe (tooling, not on the product path; scripts/gemm_algo_probe.py): the first
+// `want` algorithms hipBLASLt's heuristic offers for torch.mm's problem out[m, n] = x[m, k] ·
+// w[n, k]^T (bf16, f32 compute, the layout qz_expert_gemms uses), kept in a list; the script runs
+// each one and compares its time and bits with torch.mm's.
+namespace {
+std::vector<hipblasLtMatmulAlgo_t> g_probe_algos;
+Problem g_probe{};
+}  // namespace
+
+extern "C" {
+
+int qz_gemm_probe_algos(int64_t m, int64_t n, int64_t k, size_t workspace_bytes, int32_t want, int32_t* n_algos) {
+  const LtApi& L = api();
+  if (!L.ok) return QZ_ERR_UNAVAILABLE;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return QZ_ERR_UNAVAILABLE;
+  std::lock_guard<std::mutex> lock(g_mu);
+  hipblasLtHandle_t h = nullptr;
+  const Problem* p = nullptr;
+  int rc = problem(L, Key{dev, m, n, k, k, k, n, (uint64_t)workspace_bytes}, &h, &p);
+  if (rc) return rc;
+  g_probe = *p;
+  hipblasLtMatmulPreference_t pref = nullptr;
+  if (L.pref_create(&pref) != HIPBLAS_STATUS_SUCCESS) return QZ_ERR_UNAVAILABLE;
+  uint64_t ws = workspace_bytes;
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(want > 0 ? want : 1);
+  int returned = 0;
+  hipblasStatus_t st = L.pref_set(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &ws, sizeof(ws));
+  if (st == HIPBLAS_STATUS_SUCCESS)
+    st = L.heuristic(h, g_probe.desc, g_probe.a, g_probe.b, g_probe.c, g_probe.c, pref, (int)res.size(), res.data(),
+                     &returned);
+  L.pref_destroy(pref);
+  if (st != HIPBLAS_STATUS_SUCCESS) return QZ_ERR_UNAVAILABLE;
+  g_probe_algos.clear();
+  for (int i = 0; i < returned; ++i)
+    if (res[i].state == HIPBLAS_STATUS_SUCCESS) g_probe_algos.push_back(res[i].algo);
+  *n_algos = (int32_t)g_probe_algos.size();
+  return QZ_OK;
+}
+
+int qz_gemm_probe_run(int32_t i, const void* x, const void* w, void* out, void* workspace, size_t workspace_bytes,
+                      qz_stream_t stream) {
+  const LtApi& L = api();
+  if (!L.ok || i < 0 || i >= (int32_t)g_probe_algos.size()) return QZ_ERR_SHAPE;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return QZ_ERR_UNAVAILABLE;
+  std::lock_guard<std::mutex> lock(g_mu);
+  const float alpha = 1.0f, beta = 0.0f;
+  const hipblasStatus_t st = L.matmul(g_handles[dev], g_probe.desc, &alpha, w, g_probe.a, x, g_probe.b, &beta, out,
+                                      g_probe.c, out, g_probe.c, &g_probe_algos[i], workspace, workspace_bytes,
+                                      (hipStream_t)stream);
+  return st == HIPBLAS_STATUS_SUCCESS ? QZ_OK : QZ_ERR_UNAVAILABLE;
 }
 
 }  // extern "C"
