@@ -99,14 +99,21 @@ def _capture_layer0_inputs(model: nn.Module, layers: nn.ModuleList, batches) -> 
         raise _StopForward
 
     h = layers[0].register_forward_pre_hook(hook, with_kwargs=True)
+    ts = []
     try:
         for b in batches:
+            t0 = time.time()
             try:
                 model(**b, use_cache=False)
             except _StopForward:
                 pass
+            if awq_mod.PHASE_TIMING:  # diagnostics: per-sample wall time, synchronised
+                torch.cuda.synchronize()
+                ts.append(round(time.time() - t0, 4))
     finally:
         h.remove()
+    if ts:
+        log.info("AWQ: layer-0 capture per sample (s, synchronised): %s", ts)
     return cached
 
 
@@ -124,7 +131,9 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
     lname = next(n for n, m in model.named_modules() if m is layers)
     weights = {name: s.weights for name, (s, mod) in schemes.items() if mod is awq}
     mappings = awq.mappings or awq_mod.DEFAULT_MAPPINGS
+    t0 = time.time()
     inputs = _capture_layer0_inputs(model, layers, batches)
+    log.info("AWQ: layer-0 inputs of %d samples captured in %.2fs", len(inputs), time.time() - t0)
     mtype = model_type(model)
     stager = None
     batched: Optional[bool] = None  # per-sample layer calls run as one batched call (checked on layer 0)
@@ -219,6 +228,13 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                 # per-layer onload / offload over PCIe; save_compressed then needs no staging)
                 t0 = time.time()
                 _to_device_staged(model, device)
+                if awq_mod.PHASE_TIMING:
+                    t1 = time.time()
+                    torch.cuda.synchronize(device)
+                    t2 = time.time()
+                    torch.cuda.synchronize(device)
+                    log.info("model move: enqueue %.3fs, device sync %.3fs, second sync %.3fs", t1 - t0, t2 - t1,
+                             time.time() - t2)
                 log.info("model moved to %s in %.2fs (%.2f GB)", device, time.time() - t0,
                          sum(p.numel() * p.element_size() for p in model.parameters()) / 1e9)
             else:
@@ -261,6 +277,7 @@ def _batched_forward_ok(layer: nn.Module, inputs) -> bool:
     """Is the decoder layer's forward over the stacked samples bit-identical to its per-sample
     forwards?  (Row- and sequence-independent kernels make it so on this stack; checked once, on
     the first layer, before anything is batched.)"""
+    t0 = time.time()
     stacked = awq_mod.stack_layer_calls(inputs)
     if stacked is None:
         return False
@@ -268,8 +285,8 @@ def _batched_forward_ok(layer: nn.Module, inputs) -> bool:
     out = _layer_out(layer(*stacked[0], **stacked[1]))
     ok = all(torch.equal(out[j:j + 1].view(torch.int16), p.view(torch.int16)) if p.dtype == torch.bfloat16
              else torch.equal(out[j:j + 1], p) for j, p in enumerate(per))
-    log.info("AWQ: per-sample layer calls %s as one batched call of %d", "run" if ok else "NOT run (bits differ)",
-             len(inputs))
+    log.info("AWQ: per-sample layer calls %s as one batched call of %d (checked in %.2fs)",
+             "run" if ok else "NOT run (bits differ)", len(inputs), time.time() - t0)
     return ok
 
 
@@ -292,12 +309,22 @@ def _to_device_staged(model: nn.Module, device) -> None:
                     t.data = dst
                 else:
                     store[name] = dst
+    t0 = time.time()
     st.synchronize()
+    if awq_mod.PHASE_TIMING:
+        log.info("model move: stager %s, stream sync %.3fs", {k: round(v, 3) for k, v in st.stats.items()},
+                 time.time() - t0)
     # Unmapping host pages while DMAs run slows the DMAs ~6x on this platform (the Qwen3-4B move:
     # copy phase 1.6-1.8 s freeing as it goes vs 0.27-0.29 s deferred, profiles/r02ad_stage_probe.log),
     # and the unmapping itself takes ~0.6 s for 8 GB: it runs on a helper thread, beside the
-    # calibration work that follows.
-    threading.Thread(target=old.clear, name="qz-host-release", daemon=True).start()
+    # calibration work that follows, one tensor at a time with a GIL hand-off between them (one
+    # list.clear() holds the GIL for the whole unmapping and stalls the main thread's host work:
+    # a Python loop beside it ran +31 % slower vs +7 % freed piecewise, 8 GB of 256 MB tensors).
+    def release():
+        while old:
+            old.pop()
+            time.sleep(0)
+    threading.Thread(target=release, name="qz-host-release", daemon=True).start()
 
 
 def _onload(module: nn.Module, stager) -> Dict[tuple, torch.Tensor]:
