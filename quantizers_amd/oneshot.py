@@ -270,6 +270,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
 
 
 BATCH_LAYER_CALLS = os.environ.get("QZ_BATCH_LAYER_CALLS", "1") == "1"
+HOST_COPY = os.environ.get("QZ_HOST_COPY", "keep")  # host image of a moved model: kept with the model / "release"d
 
 
 @torch.no_grad()
@@ -316,15 +317,20 @@ def _to_device_staged(model: nn.Module, device) -> None:
                  time.time() - t0)
     # Unmapping host pages while DMAs run slows the DMAs ~6x on this platform (the Qwen3-4B move:
     # copy phase 1.6-1.8 s freeing as it goes vs 0.27-0.29 s deferred, profiles/r02ad_stage_probe.log),
-    # and the unmapping itself takes ~0.6 s for 8 GB: it runs on a helper thread, beside the
-    # calibration work that follows, one tensor at a time with a GIL hand-off between them (one
-    # list.clear() holds the GIL for the whole unmapping and stalls the main thread's host work:
-    # a Python loop beside it ran +31 % slower vs +7 % freed piecewise, 8 GB of 256 MB tensors).
-    def release():
-        while old:
-            old.pop()
-            time.sleep(0)
-    threading.Thread(target=release, name="qz-host-release", daemon=True).start()
+    # and unmapping 8 GB takes ~0.6 s during which the process's memory-map lock stalls the main
+    # thread's own GPU calls: released on a helper thread right after the move, the next
+    # synchronise waited 0.69 s on an idle device and the layer-0 capture took 0.95 s instead of
+    # 0.28 s (QZ_AWQ_PHASE_TIMING=1, scripts/gpu_r03ad.sh).  So the host image is kept with the
+    # model (the reference's model lives on the host throughout anyway) and goes when the model
+    # does; QZ_HOST_COPY=release frees it on a helper thread instead, one tensor at a time.
+    if HOST_COPY == "release":
+        def release():
+            while old:
+                old.pop()
+                time.sleep(0)
+        threading.Thread(target=release, name="qz-host-release", daemon=True).start()
+    else:
+        model._qz_host_image = old
 
 
 def _onload(module: nn.Module, stager) -> Dict[tuple, torch.Tensor]:
