@@ -222,6 +222,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         batches = _batches(dataset, num_calibration_samples, max_seq_length, device)
         if not batches:
             raise ValueError("AWQModifier needs a calibration dataset")
+        warm = _start_warmup(model, device, max(b["input_ids"].shape[1] for b in batches))
         if next(model.parameters()).device.type == "cpu" and (res is None or res.rank == 0):
             if device_resident if device_resident is not None else _fits_on_device(model, device):
                 # 288 GB of HBM: a model that fits moves to the device once and stays there (no
@@ -243,6 +244,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                 _to_device_except(model, decoder_layers(model), device)
         if res is not None:
             res.materialise_outside(model, decoder_layers(model))
+        if warm is not None:
+            warm.join()
         # MoE experts in the reference's (transformers 4.57) eager arithmetic, at grouped speed (D15)
         with eager_experts(model), fused_mlps(model), fused_rmsnorms(model), fused_rotary(model):
             for m in awqs:
@@ -267,6 +270,35 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         from .compressor import save_compressed
         save_compressed(model, output_dir)
     return model
+
+
+WARMUP = os.environ.get("QZ_WARMUP", "1") == "1"  # first-call library set-up on a thread beside the model move
+
+
+def _start_warmup(model: nn.Module, device, seq_len: int) -> Optional[threading.Thread]:
+    """First-call costs of the capture forward, paid on a helper thread while the model moves to
+    the device: the rotary embedding's f32 batched matmul ([1, head_dim / 2, 1] @ [1, 1, T]:
+    0.18 s on its first call, the BLAS library's set-up), its cat / cos / sin (0.02 s) and a bf16
+    linear (0.04 s) (`scripts/first_call_probe.py`).  Nothing it computes is used."""
+    if not WARMUP or torch.device(device).type != "cuda":
+        return None
+    cfg = getattr(model, "config", None)
+    heads = getattr(cfg, "num_attention_heads", None)
+    hd = getattr(cfg, "head_dim", None) or (getattr(cfg, "hidden_size", 0) // heads if heads else 128)
+
+    @torch.no_grad()
+    def run():
+        a = torch.ones(1, max(hd // 2, 1), 1, device=device)
+        f = (a @ torch.ones(1, 1, seq_len, device=device)).transpose(1, 2)
+        e = torch.cat((f, f), dim=-1)
+        e.cos(), e.sin()
+        x = torch.ones(16, 256, device=device, dtype=torch.bfloat16)
+        torch.nn.functional.linear(x, x)
+        torch.cuda.synchronize(device)
+
+    th = threading.Thread(target=run, name="qz-warmup", daemon=True)
+    th.start()
+    return th
 
 
 BATCH_LAYER_CALLS = os.environ.get("QZ_BATCH_LAYER_CALLS", "1") == "1"
