@@ -261,6 +261,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             return _onload(layer, stager[0])
         res.materialise_outside(model, decoder_layers(model))
         res.distribute(model, decoder_layers(model), onload, _offload)
+    if res is not None:  # helper ranks keep only the non-layer tensors they will write
+        res.release_outside(model, decoder_layers(model))
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     model.quantization_modifiers = modifiers
     model.quantization_recipe = recipe  # written next to the checkpoint as recipe.yaml

@@ -16,7 +16,8 @@ skeleton of the same architecture (``cli.load_model``).  ``Residency`` then:
   not fit the device), so the returned model stays complete there.
 
 Host memory: one model (rank 0).  Device memory per rank: its 1/N share of the checkpoint plus
-one layer.  Nothing of the compressed result crosses xGMI afterwards: each rank compresses and
+one layer, and during the pass the non-layer tensors (embeddings, lm_head -- one copy when tied --,
+final norm), which ``release_outside`` returns to meta on the ranks that do not write them.  Nothing of the compressed result crosses xGMI afterwards: each rank compresses and
 writes its own shards."""
 from __future__ import annotations
 
@@ -95,27 +96,51 @@ def _broadcast(flat: torch.Tensor, src: int) -> None:
         dist.broadcast(flat, src)
 
 
+def _alias_groups(ss: List[Slot]) -> List[int]:
+    """For each slot, the index of the first slot holding the SAME tensor object (tied weights,
+    e.g. lm_head.weight is embed_tokens.weight under tie_word_embeddings)."""
+    first: Dict[int, int] = {}
+    return [first.setdefault(id(_get(s)), i) for i, s in enumerate(ss)]
+
+
 def broadcast_slots(ss: List[Slot], device, src: int = 0) -> None:
     """Make the tensors of ``ss`` valid on every rank's ``device``: rank ``src`` provides them
-    (already on ``device``), the others receive ONE flat byte buffer and take views of it."""
-    _, rank = _world()
-    lay, off = [], 0
-    for s in ss:
+    (already on ``device``), the others receive ONE flat byte buffer and take views of it.  A
+    tensor held by several slots (tied weights) travels once, and every slot that holds it on
+    ``src`` holds one shared tensor on the other ranks too (``src``'s alias structure is sent
+    along), so ties survive on every rank and no rank's checkpoint gains an untied copy."""
+    world, rank = _world()
+    alias = _alias_groups(ss) if rank == src else None
+    if world > 1:
+        box = [alias]
+        dist.broadcast_object_list(box, src)
+        alias = box[0]
+    if len(alias) != len(ss):
+        raise ValueError(f"broadcast_slots: rank {rank} has {len(ss)} slots, rank {src} {len(alias)}")
+    lay, off = {}, 0
+    for i, s in enumerate(ss):
+        if alias[i] != i:
+            continue
         t = _get(s)
         nb = t.numel() * t.element_size()
-        lay.append((off, nb, t.shape, t.dtype))
+        lay[i] = (off, nb, t.shape, t.dtype)
         off += (nb + 255) // 256 * 256
     if off == 0:
         return
     flat = torch.empty(off, dtype=torch.uint8, device=device)
     if rank == src:
-        for s, (o, nb, _, _) in zip(ss, lay):
+        for i, (o, nb, _, _) in lay.items():
             if nb:
-                flat[o:o + nb].copy_(_get(s).detach().contiguous().reshape(-1).view(torch.uint8))
+                flat[o:o + nb].copy_(_get(ss[i]).detach().contiguous().reshape(-1).view(torch.uint8))
     _broadcast(flat, src)
     if rank != src:
-        for s, (o, nb, shape, dtype) in zip(ss, lay):
-            _set(s, flat[o:o + nb].view(dtype).view(shape))
+        for i, s in enumerate(ss):
+            if alias[i] == i:
+                o, nb, shape, dtype = lay[i]
+                _set(s, flat[o:o + nb].view(dtype).view(shape))
+            else:  # tied: the very object the first holder now has
+                m, is_buf, name = s
+                (m._buffers if is_buf else m._parameters)[name] = _get(ss[alias[i]])
 
 
 class Residency:
@@ -169,6 +194,25 @@ class Residency:
                 if t.device != self.device:
                     _set(s, t.detach().to(self.device))
         broadcast_slots(ss, self.device)
+
+    def release_outside(self, model: nn.Module, layers: nn.ModuleList) -> None:
+        """After the pass: ranks other than 0 return the non-layer tensors they will not write to
+        meta (a tensor held by several slots stays when any of its slots is owned), so a helper
+        rank ends holding only its 1/N share of the checkpoint."""
+        if self.rank == 0:
+            return
+        ss = slots(model, exclude=layers)
+        alias = _alias_groups(ss)
+        owned = {alias[i] for i, s in enumerate(ss) if self.owns(s)}
+        for i, s in enumerate(ss):
+            if alias[i] in owned:
+                continue
+            t = _get(s)
+            if alias[i] == i:
+                _set(s, torch.empty(t.shape, dtype=t.dtype, device="meta"))
+            else:
+                m, is_buf, name = s
+                (m._buffers if is_buf else m._parameters)[name] = _get(ss[alias[i]])
 
     def fetch(self, layer: nn.Module, onload) -> Optional[Dict]:
         """Layer i on every rank's device: rank 0 onloads it (``onload(layer)`` -> the host tensors

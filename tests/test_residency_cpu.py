@@ -24,7 +24,7 @@ def _port():
     return p
 
 
-def _model(meta=False):
+def _model(meta=False, tied=False):
     from quantizers_amd.quantization import QuantizationArgs, QuantizationScheme
     torch.manual_seed(0)
     ctx = torch.device("meta") if meta else torch.device("cpu")
@@ -39,7 +39,9 @@ def _model(meta=False):
             blk.up_proj = nn.Linear(64, 128, bias=True)
             blk.norm = nn.LayerNorm(64)
             m.model.layers.append(blk)
-        m.lm_head = nn.Linear(64, 32, bias=False)
+        m.lm_head = nn.Linear(64, 50 if tied else 32, bias=False)
+        if tied:  # tie_word_embeddings: lm_head.weight IS embed.weight (one Parameter)
+            m.lm_head.weight = m.model.embed.weight
     m.to(torch.bfloat16)
     sch = QuantizationScheme(targets=["Linear"], weights=QuantizationArgs(num_bits=4, type="int", symmetric=True,
                                                                           group_size=32))
@@ -47,7 +49,7 @@ def _model(meta=False):
     return m
 
 
-def _worker(rank, world, port, out_dir, q):
+def _worker(rank, world, port, out_dir, q, tied=False):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
@@ -57,13 +59,16 @@ def _worker(rank, world, port, out_dir, q):
         from test_distributed_cpu import _OraclePlan
         from quantizers_amd import compressor, residency
         compressor.CompressionPlan = _OraclePlan
-        m = _model(meta=rank != 0)
+        m = _model(meta=rank != 0, tied=tied)
         assert residency.skeleton_mode(m)
         res = residency.Residency(m, "cpu", SHARD)
         m.quantization_residency = res
         layers = m.model.layers
         res.materialise_outside(m, layers)
         res.distribute(m, layers, onload=lambda layer: None, offload=lambda layer, host: None)
+        res.release_outside(m, layers)
+        if tied:  # the tie survives the broadcasts and the release on every rank
+            assert m.lm_head.weight is m.model.embed.weight
         n_meta = sum(p.is_meta for p in m.parameters())
         compressor.save_compressed(m, out_dir, max_shard_bytes=SHARD, device="cpu")
         with pytest.raises(ValueError, match="save plan"):
@@ -73,7 +78,11 @@ def _worker(rank, world, port, out_dir, q):
         dist.destroy_process_group()
 
 
-def test_skeleton_rank_keeps_its_shards_and_save_matches_one_process(tmp_path):
+@pytest.mark.parametrize("world,tied", [(2, False), (2, True), (4, True), (8, False)])
+def test_skeleton_rank_keeps_its_shards_and_save_matches_one_process(tmp_path, world, tied):
+    """World 2 / 4 / 8 (more ranks than some shard counts: ranks that own no file, units whose
+    tensors straddle two ranks' files), tied and untied embeddings: every rank writes its own
+    shards and the directory is byte-identical to one process's."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "oracle"))
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -83,19 +92,20 @@ def test_skeleton_rank_keeps_its_shards_and_save_matches_one_process(tmp_path):
     q = ctx.Queue()
     multi = str(tmp_path / "multi")
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, multi, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, multi, q, tied)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=180) for _ in range(2)))
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=300) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res[0][0] == 0  # rank 0 keeps the whole model
-    assert 0 < res[1][0] < res[1][1]  # rank 1 holds part of it, the rest stays meta
+    assert all(0 < res[r][0] <= res[r][1] for r in range(1, world))  # helpers hold a part, the rest is meta
+    assert any(res[r][0] < res[r][1] for r in range(1, world))
     saved = compressor.CompressionPlan
     compressor.CompressionPlan = _OraclePlan
     try:
-        one = compressor.save_compressed(_model(), str(tmp_path / "one"), max_shard_bytes=SHARD, device="cpu")
+        one = compressor.save_compressed(_model(tied=tied), str(tmp_path / "one"), max_shard_bytes=SHARD, device="cpu")
     finally:
         compressor.CompressionPlan = saved
     files = sorted(os.listdir(one))
