@@ -146,8 +146,8 @@ class CompressionPlan:
     (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
     grouped launch (``ops.GroupedQuantize``: the launch ramp paid once per shape, 5 launches for
     all 252 Qwen3-4B linears; one mixed-shape launch per scheme measured 3 % slower, DESIGN §3);
-    stacked fused experts, FP8_BLOCK, NVFP4 and other
-    two-pass schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
+    NVFP4 dense units of one shape are one single-read launch (``qz_quantize_grouped_nvfp4``);
+    stacked fused experts, FP8_BLOCK and other schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
     friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
 
     def __init__(self, units: Sequence[CompressUnit], device, stager=None):
@@ -185,7 +185,7 @@ class CompressionPlan:
             if not u.stacked and ops.grouped_ok(a, w):
                 # one launch per (scheme, shape); QZ_PLAN_MIXED=1: one launch per scheme over up to
                 # 8 shapes (qz_quantize_grouped_var) -- 3 % slower on Qwen3-4B (r02q A/B)
-                key = (id(u.scheme),) if MIXED_SHAPES else (id(u.scheme), tuple(w.shape))
+                key = (id(u.scheme),) if MIXED_SHAPES and not a.is_nvfp4 else (id(u.scheme), tuple(w.shape))
                 buckets.setdefault(key, []).append((u, w))
             else:
                 self.singles.append((u, w, ops.alloc_outputs(tuple(w.shape), a, fmt, self.device), a, int_q, fmt))
@@ -582,7 +582,8 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
     ``torch.distributed`` (one process per GPU) each rank compresses only the units whose
     tensors fall in ITS shards, copies them device -> host over its own PCIe link and writes
     those files itself -- no compressed byte crosses xGMI or funnels through rank 0; rank 0 adds
-    the index and config.  Either way a shard is handed to a writer thread as soon as its bytes
+    the index and config.  The ranks must therefore share ``output_dir`` (one node, or a shared
+    filesystem): checked before anything is written (``_check_shared_dir``).  Either way a shard is handed to a writer thread as soon as its bytes
     are on the host, while later plans compress.  Every rank returns after all files exist."""
     world, rank = _dist_info()
     device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -596,6 +597,8 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
         raise ValueError(f"this model's ranks keep the tensors of a {res.world}-rank save plan with "
                          f"max_shard_bytes={res.max_shard_bytes} (oneshot(max_shard_bytes=...)); "
                          f"save_compressed was called with {world} rank(s) and {max_shard_bytes}")
+    if world > 1:
+        _check_shared_dir(output_dir, rank)
     units, raw = compression_units(model)
     plan = save_plan(units, raw, world, max_shard_bytes)
     mine = [units[i] for i in plan.units_of[rank]]
@@ -627,6 +630,33 @@ def save_compressed(model: nn.Module, output_dir: str, max_shard_bytes: int = SH
     return output_dir
 
 
+def _check_shared_dir(output_dir: str, rank: int) -> None:
+    """Every rank writes its own shards into ``output_dir``, so the directory must be the SAME
+    directory on every rank (one node, or a filesystem shared by all nodes): rank 0 drops a probe
+    file there and every rank must read it back, else the save stops before writing anything."""
+    import uuid
+    os.makedirs(output_dir, exist_ok=True)
+    box = [uuid.uuid4().hex if rank == 0 else None]
+    dist.broadcast_object_list(box, 0)
+    probe = os.path.join(output_dir, f".qz_rank_probe_{box[0]}")
+    if rank == 0:
+        with open(probe, "w") as f:
+            f.write(box[0])
+    dist.barrier()
+    try:
+        ok = open(probe).read() == box[0]
+    except OSError:
+        ok = False
+    seen: List = [None] * dist.get_world_size()
+    dist.all_gather_object(seen, ok)
+    if rank == 0:
+        os.remove(probe)
+    if not all(seen):
+        raise RuntimeError(f"save_compressed: {output_dir} is not one shared directory for all ranks (ranks "
+                           f"{[r for r, v in enumerate(seen) if not v]} cannot see rank 0's files); every rank "
+                           f"writes its own shards, so run the ranks on one node or on a shared filesystem")
+
+
 class _PlannedShardWriter:
     """Writes this rank's shards of a ``SavePlan``: tensors arrive in any grouping (plan by plan,
     then the unchanged ones); a shard is handed to a pool thread (WRITE_THREADS) once all its
@@ -651,8 +681,10 @@ class _PlannedShardWriter:
         if ready is not None:
             self.ready = ready  # one copy stream: the latest event covers every earlier copy
         for n, t in items.items():
+            if n not in self.size:  # a tensor the plan never saw would silently be lost
+                raise ValueError(f"save plan: {n} is not in the checkpoint plan")
             s = self.shard_of.get(n)
-            if s is None or n in self.held[s]:
+            if s is None or n in self.held[s]:  # another rank's shard (a straddling unit's other half)
                 continue
             nb = t.numel() * t.element_size()
             if nb != self.size[n]:

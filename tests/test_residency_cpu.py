@@ -112,3 +112,34 @@ def test_skeleton_rank_keeps_its_shards_and_save_matches_one_process(tmp_path, w
     assert files == sorted(os.listdir(multi)) and len([f for f in files if f.endswith(".safetensors")]) > 2
     for fn in files:
         assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
+
+
+def _dir_worker(rank, world, port, base, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizers_amd.compressor import _check_shared_dir
+        _check_shared_dir(os.path.join(base, "same"), rank)  # one directory: passes
+        try:
+            _check_shared_dir(os.path.join(base, f"rank{rank}"), rank)  # per-rank directories: refused
+            q.put((rank, "no error"))
+        except RuntimeError as e:
+            q.put((rank, "refused" if "not one shared directory" in str(e) else str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_save_refuses_unshared_output_dir(tmp_path):
+    """Each rank writes its own shards, so save_compressed checks that every rank sees rank 0's
+    output directory (a multi-node run without a shared filesystem stops before writing)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dir_worker, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert got == {0: "refused", 1: "refused"}, got
+    assert not [f for f in os.listdir(tmp_path / "same") if f.startswith(".qz_rank_probe")]
