@@ -10,7 +10,10 @@
  * reference-side function it replaces; INTEGRATION.md shows the ctypes stub a maintainer would
  * add.  All buffers are DEVICE pointers owned by the caller; nothing here allocates, frees or
  * synchronises.  Every call only enqueues work on `stream` (a hipStream_t, NULL = legacy
- * default stream) and is safe to call from several host threads (one device per thread).
+ * default stream) and is safe to call from several host threads (one device per thread), with
+ * two caller-side conditions: a workspace or sync region is never shared by calls that may run
+ * at the same time (the statistics workspace, qz_quantize_nvfp4's sync region: one per stream),
+ * and qz_expert_gemms serialises its callers internally (one hipBLASLt handle per device).
  *
  * Weights are bf16 (the dtype do_oneshot.py:88 loads models in), given as a batch of 2-D
  * slices: element (b, r, c) lives at w[b*ld_batch + r*ld_row + c] (elements, not bytes), so
@@ -75,7 +78,8 @@ enum {
   QZ_ERR_FORMAT = -7,       /* output format incompatible with args */
   QZ_ERR_WORKSPACE = -8,    /* workspace smaller than qz_quantize_workspace_size() */
   QZ_ERR_ALIGN = -9,        /* pointer/ld alignment violated where required */
-  QZ_ERR_UNAVAILABLE = -10  /* a runtime dependency is not loaded / refused the call (qz_expert_gemms: hipBLASLt) */
+  QZ_ERR_UNAVAILABLE = -10, /* a runtime dependency is not loaded / refused the call (qz_expert_gemms: hipBLASLt) */
+  QZ_ERR_CAPACITY = -11     /* NVFP4 single-read path: a slice needs more workgroups than are resident at once */
 };
 
 const char* qz_strerror(int code);
@@ -152,6 +156,37 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
 int64_t qz_grouped_blocks(int64_t rows, int64_t cols);
 int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* rows, const int64_t* cols,
                             const qz_args* a, int32_t out_fmt, qz_stream_t stream);
+
+/*
+ * qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4 -- NVFP4 (TENSOR_GROUP, FP4 E2M1, group 16, e4m3
+ * group scales, f32 per-slice global scale) in ONE read of the weight.  Replaces the same
+ * observer -> calculate_qparams -> quantize -> pack_fp4_to_uint8 chain as qz_quantize for the
+ * reference's NVFP4 recipes (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21,
+ * recipe_Dense_NVFP4.yaml:7-12; scheme preset NVFP4), with results identical to qz_quantize's.
+ * qz_quantize reads each slice twice (its global scale needs the whole slice's |w| maximum
+ * first); here a persistent grid holds every slice's chunks in registers until the slice's
+ * maximum is known.
+ *   qz_quantize_nvfp4: a batch of dense-row slices, slice b at w + b * ld_batch (ld_batch % 8 == 0,
+ *     w 16-B aligned); outputs as qz_quantize's (codes uint8 [batch][rows][cols/2], scales e4m3
+ *     [batch][rows][cols/16], gscale f32 [batch]).
+ *   qz_quantize_grouped_nvfp4: n independent dense [rows, cols] weights, DEVICE table of 4*n
+ *     uint64 {weights, codes, scales, global-scale pointers} (qz_quantize_grouped's layout with
+ *     the zero-point row replaced by each weight's f32 global scale).
+ * `sync`: caller-owned DEVICE region of qz_nvfp4_sync_size(slices) bytes, 16-B aligned, ZERO
+ * before its first use; every call leaves it zero.  Do not share one region between calls that
+ * may run concurrently (e.g. on two streams).  sync[0] (uint32) counts bounded waits that timed
+ * out (another kernel held CUs): the results are exact either way, only slower.
+ * QZ_ERR_CAPACITY: one slice needs more than qz_nvfp4_capacity() workgroups
+ * (qz_nvfp4_items_per_slice(rows, cols) of 64 KiB); use qz_quantize.
+ */
+size_t qz_nvfp4_sync_size(int64_t n_slices);
+int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols);
+int64_t qz_nvfp4_capacity(void);
+int qz_quantize_nvfp4(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_batch, const qz_args* a,
+                      void* q_out, void* scale_out, float* gscale_out, void* sync, size_t sync_bytes,
+                      qz_stream_t stream);
+int qz_quantize_grouped_nvfp4(int64_t n, const uint64_t* table, int64_t rows, int64_t cols, const qz_args* a,
+                              void* sync, size_t sync_bytes, qz_stream_t stream);
 
 /*
  * qz_quantize_qparams -- quantize with caller-supplied qparams (stateful observers such as the
@@ -367,6 +402,15 @@ int qz_silu_mul(const void* gate, int64_t ld_gate, const void* up, int64_t ld_up
  * per-expert `nn.functional.linear` calls (transformers 4.57 per-expert MLPs, D15) in the
  * fixed-routing forwards of an AWQ grid.  QZ_ERR_UNAVAILABLE without hipBLASLt.
  */
+/* qz_expert_gemms_library -- bind qz_expert_gemms to the hipBLASLt at `path`, which must already be
+ * loaded in the process (e.g. PyTorch's torch/lib/libhipblaslt.so); nothing is loaded here.  Once
+ * per process (the same object again returns 0; another one QZ_ERR_FORMAT).  Without this call
+ * the first qz_expert_gemms binds the loaded object with ROCm's soname "libhipblaslt.so.1".
+ * qz_expert_gemms_status -- why the last binding / GEMM call was refused ("bound: <path>" when
+ * bound).  Thread safety: qz_expert_gemms serialises its callers on one internal mutex (one
+ * hipBLASLt handle per device); several host threads on several streams are safe. */
+int qz_expert_gemms_library(const char* path);
+const char* qz_expert_gemms_status(void);
 int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride, int64_t ldw, int64_t n,
                     int64_t k, void* out, int64_t ldo, const int64_t* row0, const int64_t* row1,
                     const int32_t* expert, int32_t count, void* workspace, size_t workspace_bytes,

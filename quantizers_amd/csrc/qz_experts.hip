@@ -10,12 +10,15 @@
 // heuristic's first algorithm under the same workspace limit -- so the same kernel and the same
 // bits; the caller verifies that against torch.mm on each plan's first forward before using it.
 //
-// hipBLASLt is not linked: the functions are looked up in the process (PyTorch's bundled
-// libhipblaslt, already loaded by torch), so there is exactly one copy of the library and its
-// kernel selection is torch's.  Without it loaded the call returns QZ_ERR_UNAVAILABLE
-// (QZ_EXPERT_GEMMS_DEBUG=1 prints which step refused).
+// hipBLASLt is not linked: the functions are looked up in the copy already loaded in the process
+// (PyTorch's bundled libhipblaslt, named by the caller through qz_expert_gemms_library), so there
+// is exactly one copy of the library and its kernel selection is torch's.  Without it loaded the
+// call returns QZ_ERR_UNAVAILABLE and qz_expert_gemms_status() says why.
+//
+// Threads: one mutex serialises the GEMM issue (one hipBLASLt handle per device, whose matmul is
+// not documented thread-safe, and the problem cache): callers on several host threads / streams
+// are safe and each one's launches stay in its own stream (tests/test_moe_eager.py, 4 threads).
 #include <dlfcn.h>
-#include <link.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
 
@@ -52,51 +55,65 @@ bool debug() {
   return d;
 }
 
-// The hipBLASLt already mapped into the process (PyTorch loads its bundled copy as a dependency
-// of libtorch_hip, RTLD_LOCAL: not visible through RTLD_DEFAULT).  Prefer torch's copy when
-// more than one is mapped.
-int find_lib(struct dl_phdr_info* info, size_t, void* data) {
-  std::string* best = (std::string*)data;
-  const char* path = info->dlpi_name;
-  if (!path || !strstr(path, "libhipblaslt.so")) return 0;
-  if (best->empty() || strstr(path, "/torch/lib/")) *best = path;
-  return 0;
-}
-
-void* lib_handle() {
-  std::string path;
-  dl_iterate_phdr(find_lib, &path);
-  void* h = path.empty() ? nullptr : dlopen(path.c_str(), RTLD_NOLOAD | RTLD_LAZY);
-  if (debug()) fprintf(stderr, "qz_expert_gemms: hipBLASLt %s (%p)\n", path.empty() ? "not mapped" : path.c_str(), h);
-  return h;
-}
-
+// Which hipBLASLt: the copy already mapped into the process (PyTorch loads its bundled
+// libhipblaslt.so as a dependency of libtorch_hip, RTLD_LOCAL, so it is not visible through
+// RTLD_DEFAULT).  The caller names it: qz_expert_gemms_library(path) binds the library at `path`
+// if -- and only if -- it is already loaded (RTLD_NOLOAD: this library never loads a second
+// copy); without that call the first qz_expert_gemms binds the loaded object whose soname is
+// "libhipblaslt.so.1" (ROCm's soname).  Every refusal leaves its reason in
+// qz_expert_gemms_status().
+std::mutex g_bind_mu;
 void* g_lib = nullptr;
+bool g_bound = false;
+std::string g_status = "hipBLASLt not bound yet";
+LtApi g_api;
 
 template <class F>
-void sym(F& f, const char* name) {
-  f = reinterpret_cast<F>(g_lib ? dlsym(g_lib, name) : dlsym(RTLD_DEFAULT, name));
-  if (!f && debug()) fprintf(stderr, "qz_expert_gemms: %s not found\n", name);
+bool sym(F& f, void* h, const char* name) {
+  f = reinterpret_cast<F>(dlsym(h, name));
+  if (!f) g_status = std::string("hipBLASLt symbol missing: ") + name;
+  return f != nullptr;
+}
+
+void set_status(const std::string& m) {
+  std::lock_guard<std::mutex> lk(g_bind_mu);
+  g_status = m;
+}
+
+// caller holds g_bind_mu
+int bind(const char* path) {
+  dlerror();
+  void* h = dlopen(path, RTLD_NOLOAD | RTLD_LAZY);
+  if (!h) {
+    const char* e = dlerror();
+    g_status = std::string("hipBLASLt '") + path + "' is not loaded in this process" + (e ? std::string(": ") + e : "");
+    return QZ_ERR_UNAVAILABLE;
+  }
+  LtApi a;
+  bool ok = sym(a.create, h, "hipblasLtCreate") && sym(a.desc_create, h, "hipblasLtMatmulDescCreate") &&
+            sym(a.desc_set, h, "hipblasLtMatmulDescSetAttribute") &&
+            sym(a.layout_create, h, "hipblasLtMatrixLayoutCreate") &&
+            sym(a.pref_create, h, "hipblasLtMatmulPreferenceCreate") &&
+            sym(a.pref_set, h, "hipblasLtMatmulPreferenceSetAttribute") &&
+            sym(a.pref_destroy, h, "hipblasLtMatmulPreferenceDestroy") &&
+            sym(a.heuristic, h, "hipblasLtMatmulAlgoGetHeuristic") && sym(a.matmul, h, "hipblasLtMatmul");
+  if (!ok) {
+    dlclose(h);
+    return QZ_ERR_UNAVAILABLE;
+  }
+  a.ok = true;
+  g_api = a;
+  g_lib = h;
+  g_bound = true;
+  g_status = std::string("bound: ") + path;
+  if (debug()) fprintf(stderr, "qz_expert_gemms: %s\n", g_status.c_str());
+  return QZ_OK;
 }
 
 const LtApi& api() {
-  static LtApi a;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    g_lib = lib_handle();
-    sym(a.create, "hipblasLtCreate");
-    sym(a.desc_create, "hipblasLtMatmulDescCreate");
-    sym(a.desc_set, "hipblasLtMatmulDescSetAttribute");
-    sym(a.layout_create, "hipblasLtMatrixLayoutCreate");
-    sym(a.pref_create, "hipblasLtMatmulPreferenceCreate");
-    sym(a.pref_set, "hipblasLtMatmulPreferenceSetAttribute");
-    sym(a.pref_destroy, "hipblasLtMatmulPreferenceDestroy");
-    sym(a.heuristic, "hipblasLtMatmulAlgoGetHeuristic");
-    sym(a.matmul, "hipblasLtMatmul");
-    a.ok = a.create && a.desc_create && a.desc_set && a.layout_create && a.pref_create && a.pref_set &&
-           a.pref_destroy && a.heuristic && a.matmul;
-  });
-  return a;
+  std::lock_guard<std::mutex> lk(g_bind_mu);
+  if (!g_bound) bind("libhipblaslt.so.1");
+  return g_api;
 }
 
 // One GEMM problem: descriptors + the heuristic's algorithm, created once and kept (a few
@@ -138,7 +155,10 @@ int problem(const LtApi& L, const Key& key, hipblasLtHandle_t* handle, const Pro
   auto hit = g_handles.find(key.dev);
   if (hit == g_handles.end()) {
     hipblasLtHandle_t h = nullptr;
-    if (L.create(&h) != HIPBLAS_STATUS_SUCCESS) return QZ_ERR_UNAVAILABLE;
+    if (L.create(&h) != HIPBLAS_STATUS_SUCCESS) {
+      set_status("hipblasLtCreate failed");
+      return QZ_ERR_UNAVAILABLE;
+    }
     hit = g_handles.emplace(key.dev, h).first;
   }
   *handle = hit->second;
@@ -169,9 +189,10 @@ int problem(const LtApi& L, const Key& key, hipblasLtHandle_t* handle, const Pro
     st = L.heuristic(*handle, p.desc, p.a, p.b, p.c, p.c, pref, 1, &res, &returned);
   L.pref_destroy(pref);
   if (st != HIPBLAS_STATUS_SUCCESS || returned < 1 || res.state != HIPBLAS_STATUS_SUCCESS) {
-    if (debug())
-      fprintf(stderr, "qz_expert_gemms: heuristic status %d, %d results (m %ld n %ld k %ld)\n", (int)st, returned,
-              (long)key.m, (long)key.n, (long)key.k);
+    char msg[160];
+    snprintf(msg, sizeof msg, "hipBLASLt heuristic: status %d, %d results (m %ld n %ld k %ld)", (int)st, returned,
+             (long)key.m, (long)key.n, (long)key.k);
+    set_status(msg);
     return QZ_ERR_UNAVAILABLE;
   }
   p.algo = res.algo;
@@ -182,6 +203,26 @@ int problem(const LtApi& L, const Key& key, hipblasLtHandle_t* handle, const Pro
 }  // namespace
 
 extern "C" {
+
+int qz_expert_gemms_library(const char* path) {
+  if (!path) return QZ_ERR_NULL;
+  std::lock_guard<std::mutex> lk(g_bind_mu);
+  if (g_bound) {  // once per process: the same object again is fine, another one is refused
+    void* h = dlopen(path, RTLD_NOLOAD | RTLD_LAZY);
+    const bool same = h == g_lib;
+    if (h) dlclose(h);
+    if (!same) g_status = std::string("already bound to another hipBLASLt; refused ") + path;
+    return same ? QZ_OK : QZ_ERR_FORMAT;
+  }
+  return bind(path);
+}
+
+const char* qz_expert_gemms_status(void) {
+  static thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(g_bind_mu);
+  copy = g_status;
+  return copy.c_str();
+}
 
 int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride, int64_t ldw, int64_t n, int64_t k,
                     void* out, int64_t ldo, const int64_t* row0, const int64_t* row1, const int32_t* expert,
@@ -211,7 +252,7 @@ int qz_expert_gemms(const void* x, int64_t ldx, const void* w, int64_t w_stride,
                  ob + row0[i] * ldo, p->c, ob + row0[i] * ldo, p->c, &p->algo, workspace, workspace_bytes,
                  (hipStream_t)stream);
     if (st != HIPBLAS_STATUS_SUCCESS) {
-      if (debug()) fprintf(stderr, "qz_expert_gemms: matmul status %d (m %ld)\n", (int)st, (long)m);
+      set_status("hipblasLtMatmul status " + std::to_string((int)st) + " (m " + std::to_string((long)m) + ")");
       return QZ_ERR_UNAVAILABLE;
     }
   }

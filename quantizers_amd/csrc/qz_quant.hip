@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 
 #include "qz_device.h"
 
@@ -1063,6 +1065,151 @@ __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_
   gs[b] = bfr(bfr(1.0f / am) * 2688.0f);
 }
 
+// --------------------------------------------------------- NVFP4 single-read path
+// NVFP4 (TENSOR_GROUP) needs each slice's |w| maximum (its global scale) before any group of
+// that slice can be encoded; the two-pass path above reads every slice twice (a 403 MB fused
+// Qwen3-30B-A3B expert parameter does not fit the 256 MiB MALL, so the second read goes to HBM).
+// k_nv_hold keeps the weight ON CHIP across the per-slice maximum instead: a persistent grid
+// (as many 256-thread workgroups as are resident at once) walks "items" = 64 KiB chunks of the
+// slices, slice-major; workgroup w takes items w, w + G, w + 2G, ...  Per item it loads its
+// 16 units per lane into registers (nt loads, fully coalesced), reduces their |bf16| maximum,
+// publishes it (agent-scope atomic max on the slice's key, then an arrival add on the slice's
+// counter, both executed at the memory side, the second issued after the first returned) and
+// waits until every item of the slice has arrived; then it reads the key, forms the global scale
+// and encodes + stores its held units (process_unit, as the group path).  HBM traffic = one
+// read + one write.
+//
+// Progress: a slice has at most G items, so its items fall in at most two consecutive "rounds"
+// (item / G) and a workgroup waiting in round k only waits for items of rounds k and k + 1;
+// round k + 1's workgroups get there after finishing round k, whose waits never depend on
+// round k + 1 -- with all G workgroups resident nothing can wait forever.
+// Residency is what the occupancy query promises, not a guarantee (another kernel on the
+// device can hold CUs), so every wait is BOUNDED: after spin_ticks of the 100 MHz wall clock
+// the workgroup streams the whole slice itself to get the maximum (slow, still exact) and
+// counts the event in diag[0].  The last item of a slice to leave resets the slice's key and
+// counter, so the sync region is zero after every call (caller contract: zero before the
+// first call).
+#ifndef QZ_NV_U
+#define QZ_NV_U 16
+#endif
+constexpr int NV_U = QZ_NV_U;  // 16-B units per lane held across the wait (64 VGPRs)
+constexpr int NV_BLOCK = 256;
+constexpr int64_t NV_CHUNK = (int64_t)NV_BLOCK * NV_U;  // units per item (64 KiB of bf16 at U = 16)
+
+struct NvArgs {
+  const uint64_t* tab;  // table mode: DEVICE [4][n_slices] {weight, codes, scales, global scale}; null = batch mode
+  const uint16_t* w;    // batch mode: slice b at w + b * ld_batch (elements), dense rows
+  int64_t ld_batch;
+  void* q_out;          // batch mode outputs, dense batch-major
+  void* s_out;
+  float* gs_out;
+  int64_t n_slices;
+  int64_t units_per_slice;  // rows * cols / 8
+  int64_t items_per_slice;
+  int64_t n_items;
+  uint32_t* sync;  // [n_slices][4]: {key = |bf16| max bits, arrivals + departures, -, -}
+  uint32_t* diag;  // [0]: waits that hit the bound
+  uint64_t spin_ticks;
+  QP p;
+};
+
+__device__ __forceinline__ uint32_t absmax_bits(const uint4 v) {
+  return pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu), pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu));
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
+  __shared__ uint32_t red[NV_BLOCK / WAVE];
+  __shared__ uint32_t bc[2];
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid >> 6;
+  QP p = A.p;
+  p.kind = K_NV;
+  p.sym = 1;
+  const int64_t ups = A.units_per_slice;
+  const uint32_t n = (uint32_t)A.items_per_slice;
+  for (int64_t item = blockIdx.x; item < A.n_items; item += gridDim.x) {
+    const int64_t b = item / A.items_per_slice;
+    const int64_t base = (item - b * A.items_per_slice) * NV_CHUNK;
+    FastArgs F;
+    const uint4* src;
+    float* gs_out;
+    if constexpr (TAB) {
+      src = reinterpret_cast<const uint4*>(A.tab[b]);
+      F.q_out = reinterpret_cast<void*>(A.tab[A.n_slices + b]);
+      F.s_out = reinterpret_cast<void*>(A.tab[2 * A.n_slices + b]);
+      gs_out = reinterpret_cast<float*>(A.tab[3 * A.n_slices + b]);
+    } else {
+      src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
+      F.q_out = reinterpret_cast<uint32_t*>(A.q_out) + b * ups;
+      F.s_out = reinterpret_cast<uint8_t*>(A.s_out) + b * (ups >> 1);
+      gs_out = A.gs_out + b;
+    }
+    F.zp_out = nullptr;
+    F.scale_bytes = 1;
+    F.out_fmt = QZ_OUT_FP4_PACKED;
+    F.col_scales = nullptr;
+    uint4 v[NV_U];
+#pragma unroll
+    for (int u = 0; u < NV_U; ++u) {  // out-of-range lanes re-read the slice's last unit (never stored)
+      const int64_t un = min<int64_t>(base + u * NV_BLOCK + tid, ups - 1);
+      v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + un)));
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int u = 0; u < NV_U; ++u) m = pk_max_u16(m, absmax_bits(v[u]));
+    m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
+    if (lane == 0) red[wv] = m;
+    __syncthreads();
+    uint32_t* sy = A.sync + 4 * b;
+    if (tid == 0) {
+      m = max(max(red[0], red[1]), max(red[2], red[3]));
+      __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the max has been performed before we arrive
+      uint32_t cnt = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      uint32_t timed_out = 0;
+      if (cnt < n) {
+        const uint64_t t0 = wall_clock64();
+        for (;;) {
+          __builtin_amdgcn_s_sleep(4);
+          cnt = __hip_atomic_load(sy + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (cnt >= n) break;
+          if (wall_clock64() - t0 > A.spin_ticks) { timed_out = 1; break; }
+        }
+      }
+      bc[0] = timed_out ? 0u : __hip_atomic_fetch_max(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bc[1] = timed_out;
+    }
+    __syncthreads();
+    uint32_t key = bc[0];
+    if (bc[1]) {  // bounded wait expired: the slice's maximum from the slice itself (exact, slow)
+      uint32_t mm = 0;
+      for (int64_t un = tid; un < ups; un += NV_BLOCK) mm = pk_max_u16(mm, absmax_bits(src[un]));
+      mm = grp_max_u<WAVE>(max(mm & 0xffffu, mm >> 16));
+      if (lane == 0) red[wv] = mm;
+      __syncthreads();
+      key = max(max(red[0], red[1]), max(red[2], red[3]));
+      if (tid == 0) __hip_atomic_fetch_add(A.diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+    }
+    // global scale, k_gscale_keys' arithmetic: bf16(bf16(1 / absmax) * (448 * 6))
+    const float am = __uint_as_float(key << 16);
+    const float gs = bfr(bfr(1.0f / am) * 2688.0f);
+    if (base == 0 && tid == 0) *gs_out = gs;
+#pragma unroll
+    for (int u = 0; u < NV_U; ++u) {
+      const int64_t local = base + u * NV_BLOCK + tid;
+      process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
+    }
+    if (tid == 0) {  // depart; the slice's last leaver resets its sync words for the next call
+      const uint32_t old = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == 2u * n - 1u) {
+        __hip_atomic_store(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sy + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void store_qparams(const GP& g, int64_t gi, int scale_bytes, void* s_out, int8_t* zp_out) {
   if (scale_bytes == 2) reinterpret_cast<uint16_t*>(s_out)[gi] = (uint16_t)g.sbits;
   else reinterpret_cast<uint8_t*>(s_out)[gi] = (uint8_t)g.sbits;
@@ -1410,6 +1557,63 @@ WS ws_layout(void* base, int64_t batch, const Plan& pl) {
 }
 size_t ws_size(int64_t batch, const Plan& pl) { return ws_layout(nullptr, batch, pl).bytes; }
 
+// resident 256-thread k_nv_hold workgroups on the current device (occupancy query x CUs, at most
+// 8 per CU: MI355X_MICROARCH.md "Residency"), cached per device
+int64_t nv_capacity(bool tab) {
+  static std::mutex mu;
+  static int64_t cap[2][64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  if (cap[tab][dev] == 0) {
+    int per_cu = 0, cus = 0;
+    const hipError_t e1 = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<true>, NV_BLOCK, 0)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<false>, NV_BLOCK, 0);
+    const hipError_t e2 = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e1 != hipSuccess || e2 != hipSuccess || per_cu <= 0 || cus <= 0) return 0;
+    cap[tab][dev] = (int64_t)std::min(per_cu, 8) * cus;
+  }
+  return cap[tab][dev];
+}
+
+// the bounded wait of k_nv_hold in 100 MHz ticks (default 1 ms); QZ_NV_SPIN_TICKS is a test knob
+// that forces the exact slow path (tests/test_nvfp4_gpu.py)
+uint64_t nv_spin_ticks() {
+  static const uint64_t t = [] {
+    const char* s = getenv("QZ_NV_SPIN_TICKS");
+    return s ? (uint64_t)strtoull(s, nullptr, 10) : (uint64_t)100000;
+  }();
+  return t;
+}
+
+constexpr size_t NV_SYNC_HEAD = 256;  // diag counters, then 16 B per slice
+
+int nv_args_ok(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
+  if (!a) return QZ_ERR_NULL;
+  int rc = make_plan(a, rows, cols, pl);
+  if (rc) return rc;
+  if (pl->kind != K_NV || a->group_size != 16) return QZ_ERR_FORMAT;
+  return QZ_OK;
+}
+
+int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st) {
+  if (!sync) return QZ_ERR_NULL;
+  if (!aligned(sync, 16)) return QZ_ERR_ALIGN;
+  if (sync_bytes < NV_SYNC_HEAD + 16 * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
+  const int64_t cap = nv_capacity(tab);
+  if (cap <= 0) return (int)hipErrorInvalidDevice;
+  A.items_per_slice = cdiv(A.units_per_slice, NV_CHUNK);
+  if (A.items_per_slice > cap) return QZ_ERR_CAPACITY;
+  A.n_items = A.n_slices * A.items_per_slice;
+  A.diag = (uint32_t*)sync;
+  A.sync = (uint32_t*)((char*)sync + NV_SYNC_HEAD);
+  A.spin_ticks = nv_spin_ticks();
+  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, cap);
+  if (tab) hipLaunchKernelGGL(k_nv_hold<true>, dim3(grid), dim3(NV_BLOCK), 0, st, A);
+  else hipLaunchKernelGGL(k_nv_hold<false>, dim3(grid), dim3(NV_BLOCK), 0, st, A);
+  return launch_err();
+}
+
 }  // namespace
 
 extern "C" {
@@ -1427,6 +1631,7 @@ const char* qz_strerror(int code) {
     case QZ_ERR_WORKSPACE: return "workspace too small";
     case QZ_ERR_ALIGN: return "alignment requirement violated";
     case QZ_ERR_UNAVAILABLE: return "runtime dependency unavailable (hipBLASLt not loaded or refused the call)";
+    case QZ_ERR_CAPACITY: return "slice larger than the single-read path holds on chip (use qz_quantize)";
   }
   return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
 }
@@ -1752,6 +1957,59 @@ int qz_awq_fake_quant_batched(const void* w, int64_t batch, int64_t rows, int64_
   if (!col_scales) return QZ_ERR_NULL;
   return quantize_impl(w, batch, rows, cols, ld_row, ld_batch, a, QZ_OUT_FAKEQUANT, w_out, nullptr, nullptr, nullptr,
                        col_scales, cs_ld_batch, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+size_t qz_nvfp4_sync_size(int64_t n_slices) { return n_slices < 0 ? 0 : NV_SYNC_HEAD + 16 * (size_t)n_slices; }
+
+int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0 || cols % 16) return -1;
+  return cdiv(rows * cols / 8, NV_CHUNK);
+}
+
+int64_t qz_nvfp4_capacity(void) { return nv_capacity(false); }
+
+int qz_quantize_nvfp4(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_batch, const qz_args* a,
+                      void* q_out, void* scale_out, float* gscale_out, void* sync, size_t sync_bytes,
+                      qz_stream_t stream) {
+  if (!w || !q_out || !scale_out || !gscale_out) return QZ_ERR_NULL;
+  if (batch <= 0 || batch > 0x7fffffff) return QZ_ERR_SHAPE;
+  Plan pl;
+  int rc = nv_args_ok(a, rows, cols, &pl);
+  if (rc) return rc;
+  if (batch > 1 && (ld_batch < rows * cols || ld_batch % 8)) return QZ_ERR_SHAPE;
+  if (!aligned(w, 16) || !aligned(q_out, 4)) return QZ_ERR_ALIGN;
+  NvArgs A;
+  A.tab = nullptr;
+  A.w = (const uint16_t*)w;
+  A.ld_batch = batch > 1 ? ld_batch : rows * cols;
+  A.q_out = q_out;
+  A.s_out = scale_out;
+  A.gs_out = gscale_out;
+  A.n_slices = batch;
+  A.units_per_slice = rows * cols / 8;
+  A.p = pl.p;
+  return nv_launch(A, false, sync, sync_bytes, (hipStream_t)stream);
+}
+
+int qz_quantize_grouped_nvfp4(int64_t n, const uint64_t* table, int64_t rows, int64_t cols, const qz_args* a,
+                              void* sync, size_t sync_bytes, qz_stream_t stream) {
+  if (n == 0) return QZ_OK;
+  if (n < 0 || n > 0x7fffffff || rows <= 0 || cols <= 0) return QZ_ERR_SHAPE;
+  if (!table) return QZ_ERR_NULL;
+  if (!aligned(table, 8)) return QZ_ERR_ALIGN;
+  Plan pl;
+  int rc = nv_args_ok(a, rows, cols, &pl);
+  if (rc) return rc;
+  NvArgs A;
+  A.tab = table;
+  A.w = nullptr;
+  A.ld_batch = 0;
+  A.q_out = A.s_out = nullptr;
+  A.gs_out = nullptr;
+  A.n_slices = n;
+  A.units_per_slice = rows * cols / 8;
+  A.p = pl.p;
+  return nv_launch(A, true, sync, sync_bytes, (hipStream_t)stream);
 }
 
 int qz_quantize_qparams(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_row, int64_t ld_batch,

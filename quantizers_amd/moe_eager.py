@@ -222,10 +222,29 @@ def _direct_spec(bounds, n: int) -> list:
     return spec
 
 
+_BOUND: list = []  # [True / False] once qz_expert_gemms_library has been called
+
+
+def bind_hipblaslt(lib) -> bool:
+    """Bind qz_expert_gemms to PyTorch's own hipBLASLt (torch/lib/libhipblaslt.so, already loaded
+    by libtorch_hip) once per process; on refusal log why (qz_expert_gemms_status) and return
+    False -- the callers then keep torch.mm per expert."""
+    if not _BOUND:
+        path = os.path.join(os.path.dirname(torch.__file__), "lib", "libhipblaslt.so")
+        rc = lib.qz_expert_gemms_library(path.encode())
+        _BOUND.append(rc == 0)
+        if rc:
+            log.warning("MoE: qz_expert_gemms cannot use torch's hipBLASLt: %s; torch.mm per expert",
+                        lib.qz_expert_gemms_status().decode())
+    return _BOUND[0]
+
+
 def _run_direct(spec: list, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor) -> None:
     """The GEMMs of ``_expert_mms`` through qz_expert_gemms: one C call per stream, GIL released."""
     from . import _lib
     lib, dev = _lib.load(), x.device
+    if not bind_hipblaslt(lib):
+        raise RuntimeError(lib.qz_expert_gemms_status().decode())
     main = torch.cuda.current_stream(dev)
     ss = _side_streams(dev) if len(spec) > 1 else [main]
     for st in ss:
@@ -240,7 +259,9 @@ def _run_direct(spec: list, x: torch.Tensor, w: torch.Tensor, out: torch.Tensor)
         rc = lib.qz_expert_gemms(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), w.stride(1), w.shape[1],
                                  w.shape[2], out.data_ptr(), out.stride(0), r0.ctypes.data, r1.ctypes.data,
                                  ex.ctypes.data, len(r0), wsb.data_ptr(), _WS_BYTES, st.cuda_stream)
-        _lib.check(rc, "qz_expert_gemms")
+        if rc:
+            raise _lib.QzError(f"qz_expert_gemms: {lib.qz_strerror(rc).decode()} "
+                               f"({lib.qz_expert_gemms_status().decode()})")
     for st in ss:
         if st is not main:
             main.wait_stream(st)

@@ -48,6 +48,7 @@ def _check_dev(t: torch.Tensor, name: str):
 
 _ws_cache: Dict[Tuple[int, int], torch.Tensor] = {}
 _stats_ws_cache: Dict[Tuple[int, int], torch.Tensor] = {}
+_sync_cache: Dict[Tuple[int, int], torch.Tensor] = {}
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:
@@ -72,6 +73,37 @@ def stats_workspace(nbytes: int, device) -> torch.Tensor:
         buf = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
         _stats_ws_cache[key] = buf
     return buf
+
+
+def sync_workspace(n_slices: int, device, stream=None) -> torch.Tensor:
+    """Per-(device, stream) grow-only sync region of the NVFP4 single-read path
+    (qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4), zeroed when allocated: every call leaves it
+    zero (quantizers_amd.h), and calls on one stream never overlap, so it is shared by them."""
+    dev = torch.device(device)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    key = (dev.index or 0, st.cuda_stream)
+    nbytes = int(_lib.load().qz_nvfp4_sync_size(int(n_slices)))
+    buf = _sync_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        with torch.cuda.stream(st):
+            buf = torch.zeros(max(nbytes, 1 << 16), dtype=torch.uint8, device=dev)
+        _sync_cache[key] = buf
+    return buf
+
+
+def nvfp4_timeouts(device, stream=None) -> int:
+    """Bounded waits of the NVFP4 single-read kernel that expired on this (device, stream) sync
+    region since it was allocated (diagnostic: 0 when every slice's workgroups were resident)."""
+    dev = torch.device(device)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    buf = _sync_cache.get((dev.index or 0, st.cuda_stream))
+    return 0 if buf is None else int(buf[:4].view(torch.int32).item())
+
+
+def _nvfp4_single_read_ok(a: QuantizationArgs, out_fmt: int, geom, w: torch.Tensor) -> bool:
+    b, r, c, ld_r, ld_b = geom
+    return (a.is_nvfp4 and a.group_size == 16 and out_fmt == _lib.QZ_OUT_FP4_PACKED and ld_r == c
+            and (b == 1 or ld_b % 8 == 0) and w.data_ptr() % 16 == 0)
 
 
 def awq_stats_layout(which: str, rows: int, cols: int, group_size: int = 0) -> Dict[str, int]:
@@ -173,6 +205,14 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
     if a.is_nvfp4 and "global_scale" not in o:
         o["global_scale"] = torch.empty(max(b, 1), dtype=torch.float32, device=dev)
     lib = _lib.load()
+    if _nvfp4_single_read_ok(a, out_fmt, (b, r, c, ld_r, ld_b), w):
+        sync = sync_workspace(b, dev)
+        rc = lib.qz_quantize_nvfp4(_ptr(w), b, r, c, ld_b, ctypes.byref(ca), _ptr(o["codes"]), _ptr(o["scale"]),
+                                   _ptr(o["global_scale"]), _ptr(sync), sync.numel(), _stream())
+        if rc != _lib.QZ_ERR_CAPACITY:  # a slice too large to hold on chip: the two-pass path below
+            _lib.check(rc, "qz_quantize_nvfp4")
+            o.pop("workspace", None)
+            return o
     ws_n = lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca))
     ws = o.get("workspace")
     if ws is None or ws.numel() < ws_n:
@@ -186,9 +226,12 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
 
 
 def grouped_ok(a: QuantizationArgs, w: torch.Tensor) -> bool:
-    """True when qz_quantize_grouped covers this scheme and weight (the single-pass group path)."""
+    """True when one grouped launch covers this scheme and weight: qz_quantize_grouped (the
+    single-pass group path) or, for NVFP4, qz_quantize_grouped_nvfp4 (the single-read path)."""
     g = a.group_size or 0
-    return (a.strategy in ("group", "tensor_group") and not a.is_nvfp4 and 8 <= g <= 512 and (g & (g - 1)) == 0
+    if a.is_nvfp4 and g != 16:
+        return False
+    return (a.strategy in ("group", "tensor_group") and 8 <= g <= 512 and (g & (g - 1)) == 0
             and w.dim() == 2 and w.is_contiguous() and w.dtype == torch.bfloat16 and w.shape[1] % g == 0
             and w.data_ptr() % 16 == 0)
 
@@ -249,6 +292,10 @@ class GroupedQuantize:
                                  "tensor on one device, under a single-pass group scheme")
         shapes = [tuple(w.shape) for w in ws]
         self.mixed = len(set(shapes)) > 1
+        self.nvfp4 = a.is_nvfp4
+        if self.nvfp4 and self.mixed:
+            raise ValueError("GroupedQuantize: NVFP4 weights of one launch must share one shape")
+        self.a = a
         dev = ws[0].device
         self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
         self.ca = a.to_c()
@@ -266,9 +313,10 @@ class GroupedQuantize:
         for i, shp in enumerate(shapes):
             first.setdefault(shp, i)
         order = sorted(range(n), key=lambda i: first[shapes[i]]) if self.mixed else list(range(n))
+        last = ("global_scale" if self.nvfp4 else "zero_point")  # NVFP4: row 3 = the f32 global scale
         rows = [[ws[i].data_ptr() for i in order], [outs[i]["codes"].data_ptr() for i in order],
                 [outs[i]["scale"].data_ptr() for i in order],
-                [0 if outs[i].get("zero_point") is None else outs[i]["zero_point"].data_ptr() for i in order]]
+                [0 if outs[i].get(last) is None else outs[i][last].data_ptr() for i in order]]
         if self.mixed:
             if len(set(shapes)) > 8:
                 raise ValueError("GroupedQuantize: at most 8 distinct shapes per launch")
@@ -282,6 +330,17 @@ class GroupedQuantize:
 
     def run(self, stream=None) -> List[Dict[str, torch.Tensor]]:
         st = _P(stream.cuda_stream) if stream is not None else _stream()
+        if self.nvfp4:
+            sync = sync_workspace(self.n, self.weights[0].device, stream)
+            rc = self.lib.qz_quantize_grouped_nvfp4(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
+                                                    _ptr(sync), sync.numel(), st)
+            if rc == _lib.QZ_ERR_CAPACITY:  # weights too large to hold on chip: one two-pass launch each
+                with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                    for w, o in zip(self.weights, self.outs):
+                        quantize_weight(w, self.a, self.out_fmt, out=o)
+                return self.outs
+            _lib.check(rc, "qz_quantize_grouped_nvfp4")
+            return self.outs
         if self.mixed:
             rc = self.lib.qz_quantize_grouped_var(self.n, _ptr(self.table), ctypes.cast(self._rows, _P),
                                                   ctypes.cast(self._cols, _P), ctypes.byref(self.ca), self.out_fmt,

@@ -34,3 +34,27 @@ def test_host_only_entry_points():
     assert lib.qz_quantize_workspace_size(1, 11008, 4096, ctypes.byref(a)) > 0
     bad = _lib.QzArgs(4, 0, 1, 2, 100, 0, 0, 0)
     assert lib.qz_quantize_workspace_size(1, 16, 128, ctypes.byref(bad)) == 0
+
+
+def test_expert_gemms_binding_host_only():
+    """qz_expert_gemms binds the hipBLASLt PyTorch already loaded, by its path, never loading a
+    copy itself; a library that is not loaded is refused with a reason (no GPU needed)."""
+    import torch
+    from quantizers_amd import _lib
+    lib = _lib.load()
+    bad = os.path.join(ROOT, "no_such_dir", "libhipblaslt.so")
+    assert lib.qz_expert_gemms_library(bad.encode()) in (_lib.QZ_ERR_UNAVAILABLE, _lib.QZ_ERR_FORMAT)
+    assert b"libhipblaslt.so" in lib.qz_expert_gemms_status()
+    torch_lt = os.path.join(os.path.dirname(torch.__file__), "lib", "libhipblaslt.so")
+    assert lib.qz_expert_gemms_library(torch_lt.encode()) == 0
+    assert lib.qz_expert_gemms_status().startswith(b"bound: ")
+    assert lib.qz_expert_gemms_library(torch_lt.encode()) == 0  # idempotent
+
+
+def test_nvfp4_host_queries():
+    from quantizers_amd import _lib
+    lib = _lib.load()
+    assert lib.qz_nvfp4_sync_size(128) == 256 + 16 * 128
+    assert lib.qz_nvfp4_items_per_slice(768, 2048) == 48  # 196,608 units of 16 B / 4096 per item
+    assert lib.qz_nvfp4_items_per_slice(100, 48) == 1
+    assert lib.qz_nvfp4_items_per_slice(16, 40) == -1

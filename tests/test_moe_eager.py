@@ -205,3 +205,62 @@ def test_expert_gemms_bit_identical(cuda, n, k):
     assert rc == 0, _lib.load().qz_strerror(rc)
     torch.cuda.synchronize()
     assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+
+
+@pytest.mark.gpu
+def test_expert_gemms_four_threads(cuda):
+    """qz_expert_gemms called from 4 host threads at once, each on its own stream (the round-3 host
+    crash came from concurrent callers on one shared hipBLASLt handle; the library now serialises
+    them): threads 0-1 run the SAME problems, threads 2-3 different ones, 8 rounds each; every
+    output is bit-identical to torch.mm per expert."""
+    import threading
+    import numpy as np
+    from quantizers_amd import _lib
+    import quantizers_amd.moe_eager as me_
+    lib = _lib.load()
+    assert me_.bind_hipblaslt(lib), lib.qz_expert_gemms_status()
+    shapes = [(1536, 2048), (1536, 2048), (2048, 768), (96, 64)]
+    jobs = []
+    for t, (n, k) in enumerate(shapes):
+        g = torch.Generator().manual_seed(1000 + (t if t >= 2 else 0))
+        counts = [0, 3, 129, 700, 64, 1]
+        b = np.cumsum([0] + counts)
+        x = (torch.randn(int(b[-1]), k, generator=g) * 0.5).to(torch.bfloat16).to(cuda)
+        w = (torch.randn(len(counts), n, k, generator=g) * 0.05).to(torch.bfloat16).to(cuda)
+        want = torch.zeros(int(b[-1]), n, dtype=torch.bfloat16, device=cuda)
+        for e, c in enumerate(counts):
+            if c:
+                torch.mm(x[b[e]:b[e + 1]], w[e].t(), out=want[b[e]:b[e + 1]])
+        order = np.array([3, 1, 5, 0, 2, 4], dtype=np.int32)
+        jobs.append(dict(x=x, w=w, want=want, r0=np.ascontiguousarray(b[order]).astype(np.int64),
+                         r1=np.ascontiguousarray(b[order + 1]).astype(np.int64), ex=order, n=n, k=k,
+                         out=[torch.full_like(want, float("nan")) for _ in range(8)],
+                         ws=torch.empty(me_._WS_BYTES, dtype=torch.uint8, device=cuda),
+                         stream=torch.cuda.Stream(cuda)))
+    torch.cuda.synchronize()
+    errs = []
+    start = threading.Barrier(len(jobs))
+
+    def run(j):
+        try:
+            start.wait()
+            for o in j["out"]:
+                rc = lib.qz_expert_gemms(j["x"].data_ptr(), j["x"].stride(0), j["w"].data_ptr(), j["w"].stride(0),
+                                         j["w"].stride(1), j["n"], j["k"], o.data_ptr(), o.stride(0),
+                                         j["r0"].ctypes.data, j["r1"].ctypes.data, j["ex"].ctypes.data, len(j["ex"]),
+                                         j["ws"].data_ptr(), me_._WS_BYTES, j["stream"].cuda_stream)
+                if rc:
+                    errs.append((rc, lib.qz_expert_gemms_status()))
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=run, args=(j,)) for j in jobs]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(timeout=120)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for j in jobs:
+        for o in j["out"]:
+            assert torch.equal(o.view(torch.int16), j["want"].view(torch.int16))

@@ -1,0 +1,193 @@
+"""NVFP4 single-read path (qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4, k_nv_hold) vs the C
+oracle and vs the two-pass qz_quantize path, bit for bit.
+
+The reference's NVFP4 recipes (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21,
+recipe_Dense_NVFP4.yaml:7-12) quantize every expert / dense linear with a per-tensor global scale
+(compressed-tensors TENSOR_GROUP).  The single-read kernel holds each slice in registers across
+that per-slice maximum; these tests cover the shapes of the reference's models (Qwen3-30B-A3B
+fused experts as strided gate / up halves, dense linears of hundreds of 64 KiB items), ragged
+and one-item slices, all-zero slices, the capacity fallback, the bounded-wait fallback (forced in
+a child process) and the sync region's zero-after-call contract.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+import qref
+from quantizers_amd import _lib, ops
+from quantizers_amd.quantization import QuantizationArgs
+
+pytestmark = pytest.mark.gpu
+
+NV = dict(num_bits=4, type="float", strategy="tensor_group", group_size=16, scale_dtype="float8_e4m3fn")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class _OA:  # oracle args (qref.compress_weight reads these attributes)
+    num_bits, type, symmetric, strategy, group_size, block_structure, scale_dtype = 4, "float", True, \
+        "tensor_group", 16, None, "fp8"
+
+
+def _bits(t):
+    return t.view(torch.uint8) if t.dtype in (torch.float8_e4m3fn, torch.uint8) else t.view(torch.int32)
+
+
+def _same(a, b):
+    a, b = _bits(a.cpu()), _bits(b.cpu())
+    assert a.shape == b.shape
+    bad = a != b
+    assert not bad.any(), f"{int(bad.sum())} / {bad.numel()} differ; first {bad.nonzero()[:4].tolist()}"
+
+
+def two_pass(w: torch.Tensor, a: QuantizationArgs):
+    """The two-pass qz_quantize path (absmax pre-pass, then the group kernel) -- the comparator."""
+    b, r, c, ld_r, ld_b = ops._geom(w)
+    o = ops.alloc_outputs(tuple(w.shape), a, None, w.device)
+    lib = _lib.load()
+    ca = a.to_c()
+    ws = torch.empty(lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca)) + 256, dtype=torch.uint8,
+                     device=w.device)
+    rc = lib.qz_quantize(ops._ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), _lib.QZ_OUT_FP4_PACKED,
+                         ops._ptr(o["codes"]), ops._ptr(o["scale"]), ops._ptr(None), ops._ptr(o["global_scale"]),
+                         ops._ptr(ws), ws.numel(), ops._stream())
+    _lib.check(rc, "qz_quantize")
+    return o
+
+
+def _rand(shape, seed, scale=0.02, device="cpu"):
+    g = torch.Generator(device=device).manual_seed(seed)
+    return (torch.randn(*shape, generator=g, device=device) * scale).to(torch.bfloat16)
+
+
+def _sync_clean(dev):
+    buf = ops.sync_workspace(1, dev)
+    torch.cuda.synchronize()
+    assert int(buf[:4].view(torch.int32).item()) == 0, "bounded waits timed out (workgroups not resident)"
+    assert not buf[256:].any(), "the sync region was not left zero"
+
+
+def test_small_slices_match_oracle(cuda):
+    """Several slices, each ONE item or a ragged tail item, vs the C oracle per slice."""
+    a = QuantizationArgs(**NV)
+    for shape in [(3, 32, 128), (2, 100, 48), (4, 640, 112), (1, 16, 16)]:
+        w = torch.stack([_rand(shape[1:], seed=i, scale=0.01 * (i + 1)) for i in range(shape[0])])
+        w[0, 0, :16] = 0  # an all-zero group
+        got = ops.quantize_weight(w.to(cuda), a)
+        for i in range(shape[0]):
+            ref = qref.compress_weight(w[i], _OA)
+            _same(got["codes"][i], ref["weight_packed"])
+            _same(got["scale"][i], ref["weight_scale"])
+            _same(got["global_scale"][i:i + 1], ref["weight_global_scale"])
+    _sync_clean(cuda)
+
+
+def test_qwen3_30b_a3b_fused_experts(cuda):
+    """One Qwen3-30B-A3B MoE layer: gate_up_proj [128, 1536, 2048] as its strided gate / up halves
+    (48 items per slice) and down_proj [128, 2048, 768]: bit-identical to the two-pass path, and
+    two slices of each checked against the C oracle."""
+    a = QuantizationArgs(**NV)
+    gu = _rand((128, 1536, 2048), seed=11, device=cuda)
+    dn = _rand((128, 2048, 768), seed=12, device=cuda)
+    gu[5] *= 40  # slices with very different global scales
+    dn[7].zero_()  # an all-zero slice: global scale inf, as compressed-tensors computes it
+    for w in (gu[:, :768], gu[:, 768:], dn):
+        got = ops.quantize_weight(w, a)
+        ref = two_pass(w, a)
+        for k in ("codes", "scale", "global_scale"):
+            _same(got[k], ref[k])
+        for i in (0, 5):
+            r = qref.compress_weight(w[i].cpu().contiguous(), _OA)
+            _same(got["codes"][i], r["weight_packed"])
+            _same(got["scale"][i], r["weight_scale"])
+    _sync_clean(cuda)
+
+
+@pytest.mark.parametrize("shape", [(9728, 2560), (2560, 9728), (4096, 2560), (1024, 2560)])
+def test_grouped_dense_qwen3_4b_shapes(cuda, shape):
+    """recipe_Dense_NVFP4 on Qwen3-4B linears: one grouped launch of 6 same-shape weights (slices
+    of up to 760 items) == per-weight two-pass results; one weight also vs the C oracle."""
+    a = QuantizationArgs(**NV)
+    ws = [_rand(shape, seed=100 + i, scale=0.01 * (1 + i % 3), device=cuda) for i in range(6)]
+    gq = ops.GroupedQuantize(ws, a)
+    outs = gq.run()
+    for w, o in zip(ws, outs):
+        ref = two_pass(w, a)
+        for k in ("codes", "scale", "global_scale"):
+            _same(o[k], ref[k])
+    r = qref.compress_weight(ws[2].cpu(), _OA)
+    _same(outs[2]["codes"], r["weight_packed"])
+    _same(outs[2]["scale"], r["weight_scale"])
+    _same(outs[2]["global_scale"], r["weight_global_scale"])
+    _sync_clean(cuda)
+
+
+def test_capacity_fallback(cuda):
+    """A slice of more 64 KiB items than resident workgroups returns QZ_ERR_CAPACITY from the C
+    ABI; quantize_weight then takes the two-pass path (same results)."""
+    a = QuantizationArgs(**NV)
+    lib = _lib.load()
+    cap = lib.qz_nvfp4_capacity()
+    assert cap >= 256
+    rows = (cap + 8) * 4096 * 8 // 2048  # (cap + 8) items of 4096 units at 2048 columns
+    w = _rand((rows, 2048), seed=3, device=cuda)
+    assert lib.qz_nvfp4_items_per_slice(rows, 2048) > cap
+    o = ops.alloc_outputs(tuple(w.shape), a, None, cuda)
+    sync = ops.sync_workspace(1, cuda)
+    rc = lib.qz_quantize_nvfp4(ops._ptr(w), 1, rows, 2048, rows * 2048, ctypes.byref(a.to_c()), ops._ptr(o["codes"]),
+                               ops._ptr(o["scale"]), ops._ptr(o["global_scale"]), ops._ptr(sync), sync.numel(),
+                               ops._stream())
+    assert rc == _lib.QZ_ERR_CAPACITY
+    got = ops.quantize_weight(w, a)
+    ref = two_pass(w, a)
+    for k in ("codes", "scale", "global_scale"):
+        _same(got[k], ref[k])
+
+
+def test_argument_errors(cuda):
+    lib = _lib.load()
+    a = QuantizationArgs(**NV)
+    w = torch.zeros(64, 64, dtype=torch.bfloat16, device=cuda)
+    o = ops.alloc_outputs((64, 64), a, None, cuda)
+    sync = ops.sync_workspace(1, cuda)
+    args = lambda ca, sz=sync.numel(), sy=sync: (ops._ptr(w), 1, 64, 64, 4096, ctypes.byref(ca),  # noqa: E731
+                                                 ops._ptr(o["codes"]), ops._ptr(o["scale"]),
+                                                 ops._ptr(o["global_scale"]), ops._ptr(sy), sz, ops._stream())
+    assert lib.qz_quantize_nvfp4(*args(a.to_c(), sz=16)) == _lib.QZ_ERR_WORKSPACE
+    assert lib.qz_quantize_nvfp4(*args(a.to_c(), sy=None)) == _lib.QZ_ERR_NULL
+    mx = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
+    assert lib.qz_quantize_nvfp4(*args(mx.to_c())) == _lib.QZ_ERR_FORMAT
+    assert lib.qz_quantize_nvfp4(*args(a.to_c())) == 0
+    torch.cuda.synchronize()
+
+
+def test_bounded_wait_fallback_child():
+    """QZ_NV_SPIN_TICKS=0: every workgroup that is not the last of its slice gives up waiting at
+    once and streams the whole slice for its maximum -- the exact slow path.  Run in a child
+    process (the knob is read once per process); the child checks bit-identity with the two-pass
+    path and that the timeout counter moved."""
+    code = r"""
+import sys, torch
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+from tests.test_nvfp4_gpu import two_pass, _rand, _same, NV
+from quantizers_amd import ops
+from quantizers_amd.quantization import QuantizationArgs
+a = QuantizationArgs(**NV)
+dev = torch.device("cuda:0")
+w = _rand((16, 768, 2048), seed=21, device=dev)
+got = ops.quantize_weight(w, a)
+ref = two_pass(w, a)
+for k in ("codes", "scale", "global_scale"):
+    _same(got[k], ref[k])
+torch.cuda.synchronize()
+n = ops.nvfp4_timeouts(dev)
+assert n > 0, n
+print("timeouts", n)
+""" % (ROOT, os.path.join(ROOT, "oracle"))
+    env = dict(os.environ, QZ_NV_SPIN_TICKS="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "timeouts" in r.stdout
