@@ -46,6 +46,7 @@ import time
 import torch
 import torch.distributed as dist
 
+T_START = time.perf_counter()  # after `import torch`: the phase budget starts here
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -190,9 +191,76 @@ def other_configs(ops, QuantizationArgs, dev, gen):
     npar = 48 * 128 * 3 * 768 * 2048
     t = _timed(moe_pass, reps=2)
     res["qwen3_30b_a3b_experts_mxfp4"] = {"params": npar, "ms": t * 1e3, "params_per_s": npar / t,
-                                          "alg_GBps": npar * (2 + 0.5 + 1 / 32) / t / 1e9}
+                                          "alg_GBps": npar * (2 + 0.5 + 1 / 32) / t / 1e9,
+                                          "frac": npar * (2 + 0.5 + 1 / 32) / t / 1e9 / HBM_PEAK_GBS}
+    res["qwen3_30b_a3b_experts_nvfp4"] = nvfp4_experts_leg(ops, QuantizationArgs, layers, dev)
     del layers
     torch.cuda.empty_cache()
+    return res
+
+
+NV_B_PER_PARAM = 2 + 0.5 + 1 / 16  # NVFP4: read 2 B + packed E2M1 0.5 B + one e4m3 scale per 16
+
+
+def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
+    """The reference's own Qwen3-30B-A3B recipe (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21
+    -> NVFP4: E2M1 codes, e4m3 group-16 scales, one f32 global scale per expert linear): every
+    expert weight of the 48 layers (4 resident fused layers rotated, as the MXFP4 leg) through
+    the single-read kernel (qz_quantize_nvfp4 -> k_nv_hold, one launch per fused parameter),
+    outputs preallocated.  HIP events on the launch stream around one whole pass (144 launches
+    back to back); the two-pass qz_quantize path timed the same way beside it.  Algorithmic bytes
+    per param = 2.5625 (+ 4 B per expert linear)."""
+    import ctypes
+    from quantizers_amd import _lib
+    nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16,
+                          scale_dtype="float8_e4m3fn")
+    views = [(li, j, w) for li, (gu, dn) in enumerate(layers) for j, w in enumerate((gu[:, :768], gu[:, 768:], dn))]
+    outs = {(li, j): ops.alloc_outputs(tuple(w.shape), nv, None, dev) for li, j, w in views}
+    lib = _lib.load()
+    ca = nv.to_c()
+    ws = torch.empty(lib.qz_quantize_workspace_size(128, 2048, 768, ctypes.byref(ca)) + 256, dtype=torch.uint8,
+                     device=dev)
+
+    def single():
+        for li in range(48):
+            for lj, j, w in views[(li % 4) * 3:(li % 4) * 3 + 3]:
+                ops.quantize_weight(w, nv, out=outs[(lj, j)])
+
+    def two_pass():
+        for li in range(48):
+            for lj, j, w in views[(li % 4) * 3:(li % 4) * 3 + 3]:
+                b, r, c, ld_r, ld_b = ops._geom(w)
+                o = outs[(lj, j)]
+                rc = lib.qz_quantize(ops._ptr(w), b, r, c, ld_r, ld_b, ctypes.byref(ca), _lib.QZ_OUT_FP4_PACKED,
+                                     ops._ptr(o["codes"]), ops._ptr(o["scale"]), ops._ptr(None),
+                                     ops._ptr(o["global_scale"]), ops._ptr(ws), ws.numel(), ops._stream())
+                _lib.check(rc, "qz_quantize")
+    npar = 48 * 128 * 3 * 768 * 2048
+    nb = npar * NV_B_PER_PARAM + 48 * 3 * 128 * 4
+    res = {"params": npar, "alg_bytes": nb, "kernel": "k_nv_hold<false> (qz_quantize_nvfp4)",
+           "recipe": "reference configs/recipes/recipe_MoE_RTN_NVFP4.yaml (scheme NVFP4)",
+           "timing": "HIP events around one whole pass (144 launches back to back), best of 3"}
+    st = torch.cuda.current_stream(dev)
+    for name, fn in (("single_read", single), ("two_pass", two_pass)):
+        fn()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            fn()
+            e1.record(st)
+            torch.cuda.synchronize()
+            best = e0.elapsed_time(e1) * 1e-3 if best is None else min(best, e0.elapsed_time(e1) * 1e-3)
+        gbps = nb / best / 1e9
+        leg = {"ms": best * 1e3, "params_per_s": npar / best, "alg_GBps": gbps, "frac": gbps / HBM_PEAK_GBS,
+               "read_frac": npar * 2 / best / 1e9 / HBM_PEAK_GBS}
+        if name == "single_read":
+            res.update(leg)
+            res["bounded_wait_timeouts"] = ops.nvfp4_timeouts(dev)
+        else:
+            res["two_pass_qz_quantize"] = leg
+    del outs
     return res
 
 
@@ -670,6 +738,15 @@ def main():
     from quantizers_amd.compressor import CompressionPlan, compression_units
     from quantizers_amd.quantization import QuantizationArgs
 
+    phases = {}  # per-rank wall seconds by phase (max over ranks goes in the line)
+    t_phase = [T_START]
+
+    def stamp(name):
+        now = time.perf_counter()
+        phases[name] = phases.get(name, 0.0) + now - t_phase[0]
+        t_phase[0] = now
+
+    stamp("start_to_device")
     torch.manual_seed(1234 + rank)
     model = build_model(dev)
     units, _ = compression_units(model)
@@ -698,9 +775,11 @@ def main():
             _all_reduce_max(wall)
         return wall.item(), e0.elapsed_time(e1)
 
+    stamp("model_and_plan")
     for _ in range(args.warmup):
         plan.run(stream)
     el, ev_ms = region(args.steps)
+    stamp("headline")
     if args.profile_only:
         return
 
@@ -715,9 +794,11 @@ def main():
         nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
                                                          for t in o.values() if t is not None)
         us = e0.elapsed_time(e1) * 1e3
+        rb = sum(w.numel() * 2 for _, w in part)
         per_launch.append({"shapes": sorted({f"{r}x{c}" for r, c in gq.shapes}), "weights": gq.n,
-                           "us": us, "alg_bytes": nb,
-                           "GBps": nb / (us * 1e-6) / 1e9})
+                           "us": us, "alg_bytes": nb, "read_bytes": rb,
+                           "GBps": nb / (us * 1e-6) / 1e9, "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                           "read_frac": rb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS})
 
     checks = []
     if rank == 0:  # the measured outputs of one module per shape, checked in the CPU leg
@@ -728,8 +809,11 @@ def main():
     # multi-GPU legs (BASELINE.md §2 multi-GPU row; north star: RCCL all-gather over xGMI), run at
     # every N so the driver's 1/2/4/8-GPU lines carry comparable fields
     ranks_seen = dist.get_world_size() if world > 1 else 1
+    stamp("per_launch_and_checks")
     strong = strong_model_leg(units, dev, stream, world, rank, steps=10 if backend == "nccl" else 2)
+    stamp("strong_scaling_leg")
     row_sharded = row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank)
+    stamp("row_sharded_leg")
     # PCIe-inclusive rate (not the headline): what save_compressed pays per model on one GPU --
     # the same plan, then every output tensor copied to pinned host memory (_HostCopier: side
     # stream, one device->host copy per tensor).  One warm run first (pinned-host allocator).
@@ -773,9 +857,18 @@ def main():
         other["minimax_m2_1_mixedprec_sharded"] = minimax_pass(ops, QuantizationArgs, dev, gen, world, rank)
         extras["other_configs"] = other
 
+    stamp("extras")
     cpu, ok = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, ok = cpu_baseline(args.cpu_seconds, checks + ([cpu_check] if cpu_check else []))
+    stamp("cpu_baseline")
+    names = sorted(phases)
+    pt = torch.tensor([phases[k] for k in names], device=dev, dtype=torch.float64)
+    if world > 1:
+        _all_reduce_max(pt)
+    phase_max = dict(zip(names, [round(v, 3) for v in pt.tolist()]))
+    print(f"bench.py rank {rank}/{world}: phase seconds {json.dumps({k: round(v, 3) for k, v in phases.items()})}",
+          file=sys.stderr, flush=True)
 
     if rank == 0:
         value = world * params_step * args.steps / el
@@ -812,7 +905,13 @@ def main():
                        "parallelism": f"weight-shard dp{world}"},
             "hbm_GBps_step": world * alg_step * args.steps / el / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         # the north star's "HBM-read roofline" reading: weight bytes read only
+                         "read_frac": params_step * 2 * args.steps / ev_s / 1e9 / HBM_PEAK_GBS,
+                         "read_achieved": params_step * 2 * args.steps / ev_s / 1e9,
+                         "frac_definition": "frac = algorithmic read + write bytes (SURVEY §8d) / kernel time / "
+                                            "8 TB/s; read_frac = weight bytes read / kernel time / 8 TB/s",
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kernel_name(True, 36 * 9728 * 2560 * 2),
                          "kernel_ms_mean": ev_ms / (args.steps * launches_step),
                          "launches_per_step": launches_step, "alg_bytes_per_step": alg_step,
@@ -828,6 +927,8 @@ def main():
             "row_sharded_synthetic_11008x4096": row_sharded,
             "strong_scaling_qwen3_4b_sharded": strong,
             "pcie_inclusive": pcie,
+            "phase_seconds_max_rank": phase_max,
+            "wall_seconds_max_rank": round(sum(phase_max.values()), 3),
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
