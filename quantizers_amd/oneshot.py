@@ -27,6 +27,7 @@ from .dense_mlp import fused_mlps
 from .dense_norm import fused_rmsnorms
 from .rotary import fused_rotary
 from .moe_eager import eager_experts
+from .patching import bmm_guard
 from .model import checkpoint_name, decoder_layers, iter_linears, model_type
 from .quantization import QuantizationScheme
 from .recipe import AWQModifier, QuantizationModifier, match_any, match_precedence, parse_recipe
@@ -247,7 +248,10 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         if warm is not None:
             warm.join()
         # MoE experts in the reference's (transformers 4.57) eager arithmetic, at grouped speed (D15)
-        with eager_experts(model), fused_mlps(model), fused_rmsnorms(model), fused_rotary(model):
+        with bmm_guard(), eager_experts(model), fused_mlps(model) as n_mlp, fused_rmsnorms(model) as n_norm, \
+                fused_rotary(model) as n_rot:
+            _log_swaps(model, {"SiLU·up (dense_mlp)": n_mlp, "128-wide RMSNorm (dense_norm)": n_norm,
+                               "rotary embedding (rotary)": n_rot})
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
                                 stateful_observers, residency=res, seconds=layer_seconds)
@@ -272,6 +276,26 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
         from .compressor import save_compressed
         save_compressed(model, output_dir)
     return model
+
+
+# model types whose transformers forwards the dense swaps restate (D16): for these a swap that
+# does not engage means transformers' code changed -- the AWQ pass stays exact, only slower
+_SWAP_MODEL_TYPES = ("qwen3",)
+
+
+def _log_swaps(model: nn.Module, counts: Dict[str, int]) -> None:
+    """One line per D16 forward swap: how many modules / functions it engaged; a warning for each
+    swap that engaged nothing on a model type it was written for (patching.same_code found no
+    bytecode-equal forward, e.g. after a transformers upgrade)."""
+    mtype = getattr(getattr(model, "config", None), "model_type", None)
+    for name, n in counts.items():
+        if n:
+            log.info("AWQ pass: %s swap engaged on %d module(s)", name, n)
+        elif mtype in _SWAP_MODEL_TYPES:
+            log.warning("AWQ pass: %s swap did NOT engage on this %s model (no forward is bytecode-equal to the "
+                        "transformers code it restates); the model's own forward runs -- exact, slower", name, mtype)
+        else:
+            log.info("AWQ pass: %s swap not applicable to model type %s", name, mtype)
 
 
 WARMUP = os.environ.get("QZ_WARMUP", "1") == "1"  # first-call library set-up on a thread beside the model move
