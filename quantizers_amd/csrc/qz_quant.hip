@@ -759,6 +759,9 @@ __device__ __forceinline__ void fq_load_tile(uint4 (&v)[U], const uint4* src, in
 #ifndef QZ_FQ_ST_AUX
 #define QZ_FQ_ST_AUX 16  // cache policy of the buffer stores: sc1 (gfx950 CPol SC1 = 16)
 #endif
+#ifndef QZ_FQ_LD_AUX
+#define QZ_FQ_LD_AUX 0  // cache policy of the one-tile fake-quant's weight loads (A/B knob; 2 = nt)
+#endif
 #ifndef QZ_FQ_BUF
 #define QZ_FQ_BUF 1  // 1: one-tile waves load / store through wave-uniform buffer descriptors (A/B knob)
 #endif
@@ -803,7 +806,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
         0x00020000);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], 0));
+      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], QZ_FQ_LD_AUX));
   } else {
     fq_load_tile<NT, U>(v, src, rblk * U * FQ_TILES, rows, upr, cuc);
   }
@@ -1089,10 +1092,13 @@ __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_
 // counts the event in diag[0].  The last item of a slice to leave resets the slice's key and
 // counter, so the sync region is zero after every call (caller contract: zero before the
 // first call).
-#ifndef QZ_NV_U
-#define QZ_NV_U 16
+#ifndef QZ_NV_PIPE
+#define QZ_NV_PIPE 1  // 1: the next item's loads are in flight while the current item waits (A/B knob)
 #endif
-constexpr int NV_U = QZ_NV_U;  // 16-B units per lane held across the wait (64 VGPRs)
+#ifndef QZ_NV_U
+#define QZ_NV_U (QZ_NV_PIPE ? 8 : 16)
+#endif
+constexpr int NV_U = QZ_NV_U;  // 16-B units per lane per item (x2 with the pipeline: 64 VGPRs)
 constexpr int NV_BLOCK = 256;
 constexpr int64_t NV_CHUNK = (int64_t)NV_BLOCK * NV_U;  // units per item (64 KiB of bf16 at U = 16)
 
@@ -1107,11 +1113,23 @@ struct NvArgs {
   int64_t units_per_slice;  // rows * cols / 8
   int64_t items_per_slice;
   int64_t n_items;
-  uint32_t* sync;  // [n_slices][4]: {key = |bf16| max bits, arrivals + departures, -, -}
+  uint32_t* sync;  // [n_slices][NV_SYNC_STRIDE]: {key = |bf16| max bits, arrivals + departures, unused...}
   uint32_t* diag;  // [0]: waits that hit the bound
   uint64_t spin_ticks;
   QP p;
 };
+
+// the current value of a sync word, read AT THE MEMORY SIDE: a compare-exchange that always fails
+// (no sync word ever holds 0xffffffff).  A relaxed agent-scope atomic load, or an idempotent RMW
+// (which LLVM turns into one), compiles to a global_load ... sc1 that can be served from this
+// XCD's L2 copy of the line while another XCD's atomics update it (per-XCD L2s are not coherent).
+__device__ __forceinline__ uint32_t sync_read(uint32_t* p) {
+  uint32_t e = 0xffffffffu;
+  __hip_atomic_compare_exchange_strong(p, &e, 0xfffffffeu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return e;
+}
+constexpr int NV_SYNC_STRIDE = 16;  // uint32 words per slice: one 64-B line each
 
 __device__ __forceinline__ uint32_t absmax_bits(const uint4 v) {
   return pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu), pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu));
@@ -1127,9 +1145,25 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
   p.sym = 1;
   const int64_t ups = A.units_per_slice;
   const uint32_t n = (uint32_t)A.items_per_slice;
+  auto load = [&](uint4 (&v)[NV_U], int64_t it) {  // out-of-range lanes re-read the slice's last unit
+    const int64_t bb = it / A.items_per_slice;
+    const int64_t b0 = (it - bb * A.items_per_slice) * NV_CHUNK;
+    const uint4* s0 = TAB ? reinterpret_cast<const uint4*>(A.tab[bb]) : reinterpret_cast<const uint4*>(A.w + bb * A.ld_batch);
+#pragma unroll
+    for (int u = 0; u < NV_U; ++u) {
+      const int64_t un = min<int64_t>(b0 + u * NV_BLOCK + tid, ups - 1);
+      v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + un)));
+    }
+  };
+  if ((int64_t)blockIdx.x >= A.n_items) return;
+  uint4 v[NV_U];
+  load(v, blockIdx.x);
   for (int64_t item = blockIdx.x; item < A.n_items; item += gridDim.x) {
     const int64_t b = item / A.items_per_slice;
     const int64_t base = (item - b * A.items_per_slice) * NV_CHUNK;
+    const int64_t next = item + gridDim.x;
+    uint4 nv[NV_U];
+    if (QZ_NV_PIPE && next < A.n_items) load(nv, next);  // in flight while this item waits
     FastArgs F;
     const uint4* src;
     float* gs_out;
@@ -1148,35 +1182,30 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
     F.scale_bytes = 1;
     F.out_fmt = QZ_OUT_FP4_PACKED;
     F.col_scales = nullptr;
-    uint4 v[NV_U];
-#pragma unroll
-    for (int u = 0; u < NV_U; ++u) {  // out-of-range lanes re-read the slice's last unit (never stored)
-      const int64_t un = min<int64_t>(base + u * NV_BLOCK + tid, ups - 1);
-      v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + un)));
-    }
     uint32_t m = 0;
 #pragma unroll
     for (int u = 0; u < NV_U; ++u) m = pk_max_u16(m, absmax_bits(v[u]));
     m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
     if (lane == 0) red[wv] = m;
     __syncthreads();
-    uint32_t* sy = A.sync + 4 * b;
+    uint32_t* sy = A.sync + NV_SYNC_STRIDE * b;
     if (tid == 0) {
       m = max(max(red[0], red[1]), max(red[2], red[3]));
-      __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the max has been performed before we arrive
-      uint32_t cnt = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+      // the arrival add depends on the max's RETURNED value (its top bit is never set): the max
+      // has been performed at the memory side before this workgroup counts as arrived
+      const uint32_t old = __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t cnt = __hip_atomic_fetch_add(sy + 1, 1u + (old >> 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
       uint32_t timed_out = 0;
       if (cnt < n) {
         const uint64_t t0 = wall_clock64();
         for (;;) {
-          __builtin_amdgcn_s_sleep(4);
-          cnt = __hip_atomic_load(sy + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_s_sleep(2);
+          cnt = sync_read(sy + 1);
           if (cnt >= n) break;
           if (wall_clock64() - t0 > A.spin_ticks) { timed_out = 1; break; }
         }
       }
-      bc[0] = timed_out ? 0u : __hip_atomic_fetch_max(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bc[0] = timed_out ? 0u : sync_read(sy);
       bc[1] = timed_out;
     }
     __syncthreads();
@@ -1205,6 +1234,14 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
       if (old == 2u * n - 1u) {
         __hip_atomic_store(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sy + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (next < A.n_items) {
+      if constexpr (QZ_NV_PIPE) {
+#pragma unroll
+        for (int u = 0; u < NV_U; ++u) v[u] = nv[u];
+      } else {
+        load(v, next);
       }
     }
   }
@@ -1586,7 +1623,7 @@ uint64_t nv_spin_ticks() {
   return t;
 }
 
-constexpr size_t NV_SYNC_HEAD = 256;  // diag counters, then 16 B per slice
+constexpr size_t NV_SYNC_HEAD = 256;  // diag counters, then one 64-B line per slice
 
 int nv_args_ok(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
   if (!a) return QZ_ERR_NULL;
@@ -1599,7 +1636,7 @@ int nv_args_ok(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
 int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st) {
   if (!sync) return QZ_ERR_NULL;
   if (!aligned(sync, 16)) return QZ_ERR_ALIGN;
-  if (sync_bytes < NV_SYNC_HEAD + 16 * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
+  if (sync_bytes < NV_SYNC_HEAD + 4 * NV_SYNC_STRIDE * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
   const int64_t cap = nv_capacity(tab);
   if (cap <= 0) return (int)hipErrorInvalidDevice;
   A.items_per_slice = cdiv(A.units_per_slice, NV_CHUNK);
@@ -1959,7 +1996,9 @@ int qz_awq_fake_quant_batched(const void* w, int64_t batch, int64_t rows, int64_
                        col_scales, cs_ld_batch, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
-size_t qz_nvfp4_sync_size(int64_t n_slices) { return n_slices < 0 ? 0 : NV_SYNC_HEAD + 16 * (size_t)n_slices; }
+size_t qz_nvfp4_sync_size(int64_t n_slices) {
+  return n_slices < 0 ? 0 : NV_SYNC_HEAD + 4 * NV_SYNC_STRIDE * (size_t)n_slices;
+}
 
 int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols) {
   if (rows <= 0 || cols <= 0 || cols % 16) return -1;

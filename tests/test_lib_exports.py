@@ -54,7 +54,7 @@ def test_expert_gemms_binding_host_only():
 def test_nvfp4_host_queries():
     from quantizers_amd import _lib
     lib = _lib.load()
-    assert lib.qz_nvfp4_sync_size(128) == 256 + 16 * 128
+    assert lib.qz_nvfp4_sync_size(128) == 256 + 64 * 128
     assert lib.qz_nvfp4_items_per_slice(768, 2048) == 48  # 196,608 units of 16 B / 4096 per item
     assert lib.qz_nvfp4_items_per_slice(100, 48) == 1
     assert lib.qz_nvfp4_items_per_slice(16, 40) == -1
