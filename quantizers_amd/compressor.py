@@ -137,10 +137,6 @@ def compression_units(model: nn.Module) -> Tuple[List[CompressUnit], Dict[str, t
     return units, raw
 
 
-MIXED_SHAPES = os.environ.get("QZ_PLAN_MIXED", "0") == "1"  # measured slower, see DESIGN §3
-PLAN_STREAMS = int(os.environ.get("QZ_PLAN_STREAMS", "1"))  # grouped launches spread over streams (A/B knob)
-
-
 class CompressionPlan:
     """Prepared kernel launches for a set of compression units whose weights are on ``device``
     (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
@@ -153,8 +149,6 @@ class CompressionPlan:
     def __init__(self, units: Sequence[CompressUnit], device, stager=None):
         self.device = torch.device(device)
         self.grouped = []  # (GroupedQuantize, [(unit, weight)], args, int_q, fmt)
-        self._side = None  # side streams / events of a multi-stream run()
-        self._ev = None
         self.singles = []  # (unit, weight, preallocated outputs, args, int_q, fmt)
         buckets: Dict[tuple, list] = {}
         self.params = 0
@@ -183,9 +177,9 @@ class CompressionPlan:
             self.params += w.numel()
             int_q, fmt = ops._compress_plan(a, u.scheme.input_activations is not None)
             if not u.stacked and ops.grouped_ok(a, w):
-                # one launch per (scheme, shape); QZ_PLAN_MIXED=1: one launch per scheme over up to
-                # 8 shapes (qz_quantize_grouped_var) -- 3 % slower on Qwen3-4B (r02q A/B)
-                key = (id(u.scheme),) if MIXED_SHAPES and not a.is_nvfp4 else (id(u.scheme), tuple(w.shape))
+                # one launch per (scheme, shape); one mixed-shape launch per scheme
+                # (qz_quantize_grouped_var) measured 3 % slower on Qwen3-4B (r02q A/B)
+                key = (id(u.scheme), tuple(w.shape))
                 buckets.setdefault(key, []).append((u, w))
             else:
                 self.singles.append((u, w, ops.alloc_outputs(tuple(w.shape), a, fmt, self.device), a, int_q, fmt))
@@ -229,22 +223,8 @@ class CompressionPlan:
         main = stream if stream is not None else torch.cuda.current_stream(self.device)
         if self._ready is not None:
             main.wait_event(self._ready)
-        n_st = min(PLAN_STREAMS, len(self.grouped))
-        if n_st > 1:  # launches alternate over streams: one launch's drain overlaps the next's fill
-            if self._side is None or len(self._side) != n_st - 1:
-                self._side = [torch.cuda.Stream(self.device) for _ in range(n_st - 1)]
-                self._ev = [torch.cuda.Event() for _ in range(n_st)]
-            self._ev[0].record(main)
-            for sd in self._side:
-                sd.wait_event(self._ev[0])
-            for i, (gq, *_) in enumerate(self.grouped):
-                gq.run(main if i % n_st == 0 else self._side[i % n_st - 1])
-            for sd, ev in zip(self._side, self._ev[1:]):
-                ev.record(sd)
-                main.wait_event(ev)
-        else:
-            for gq, *_ in self.grouped:
-                gq.run(main)
+        for gq, *_ in self.grouped:  # one stream: spreading the launches over 2-3 streams measured
+            gq.run(main)             # slower (r02r A/B)
         if self.singles:
             with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device)):
                 for u, w, o, a, int_q, fmt in self.singles:

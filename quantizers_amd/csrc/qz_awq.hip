@@ -261,96 +261,6 @@ __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int
   }
 }
 
-#ifndef QZ_STATS_WALK
-#define QZ_STATS_WALK 0  // 1: stats_walk_u (uniform row addresses, pinned prefetch); 0: stats_walk (A/B knob)
-#endif
-#ifndef QZ_STATS_AUX
-#define QZ_STATS_AUX 0  // stats_walk_u: cache-policy bits of the buffer loads (A/B knob)
-#endif
-#ifndef QZ_STATS_DIST
-#define QZ_STATS_DIST 2  // stats_walk_u: batches in flight ahead of the one being summed (1 or 2)
-#endif
-// The same walk with the row part of every address wave-uniform: the lane's (row q, column c0)
-// offset is a constant 32-bit VGPR (bytes from the matrix base; the host keeps q * ld + c0 <
-// 2^31 elements), the batch's row base an SGPR pair,
-// so a full batch costs no VALU for addresses (global_load ... voff, s[base]); only the last,
-// partial batch clamps rows per lane.  The next DIST batches' loads are issued before the
-// current batch is summed, pinned there by a scheduling barrier (the compiler otherwise sinks
-// them towards the loop end, which leaves one batch in flight for half the loop), and DIST + 1
-// register sets are used in turn (no copies).  Same rows, same order per slot as stats_walk.
-template <int S, int SNB, int DIST, typename F>
-__device__ __forceinline__ void stats_walk_u(const uint16_t* base, int64_t c0, int64_t ld, int64_t rb, int q,
-                                             int64_t r1, F&& f) {
-  if (rb >= r1) return;
-  constexpr int64_t STEP = (int64_t)SNB * S;
-  const int64_t nfull = (r1 - rb) / STEP;  // full batches (uniform): every row of one is < r1
-  const int64_t nb = nfull + ((r1 - rb) % STEP ? 1 : 0);
-  const uint32_t rowb = (uint32_t)ld * 2u, cb = (uint32_t)c0 * 2u, voff = (uint32_t)q * rowb + cb;
-  auto load = [&](uint4 (&d)[SNB], int64_t k) {
-    const int64_t r = rb + k * STEP;
-    // one buffer descriptor per batch, built from wave-uniform values only (SGPRs); rows of the
-    // batch at 32-bit offsets from it (the caller keeps STEP * ld * 2 < 2^31)
-    const uint64_t pa = (uint64_t)(base + r * ld);
-    const uint64_t pu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)pa) |
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) << 32);
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)pu, 0, 0x7fffffff, 0x00020000);
-    if (k < nfull) {
-#pragma unroll
-      for (int j = 0; j < SNB; ++j)
-        d[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             rs, voff, __builtin_amdgcn_readfirstlane((uint32_t)(j * S) * rowb),
-                                             QZ_STATS_AUX));
-    } else {
-      const uint32_t rem = (uint32_t)(r1 - r);  // rows left (< STEP); past them: the last row again
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) {
-        const uint32_t rr = std::min((uint32_t)(q + j * S), rem - 1u);
-        d[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, rr * rowb + cb, 0, QZ_STATS_AUX));
-      }
-    }
-  };
-  auto use = [&](uint4 (&d)[SNB], int64_t k) {
-    if (k < nfull) {
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) f(d[j], true);
-    } else {
-      const uint32_t rem = (uint32_t)(r1 - rb - k * STEP);
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) f(d[j], (uint32_t)(q + j * S) < rem);
-    }
-  };
-  uint4 a[SNB], b[SNB], c[SNB];
-  load(a, 0);
-  if constexpr (DIST == 1) {
-    for (int64_t k = 0;; k += 2) {
-      if (k + 1 < nb) load(b, k + 1);
-      __builtin_amdgcn_sched_barrier(0);
-      use(a, k);
-      if (k + 1 >= nb) return;
-      if (k + 2 < nb) load(a, k + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      use(b, k + 1);
-      if (k + 2 >= nb) return;
-    }
-  } else {
-    if (nb > 1) load(b, 1);
-    for (int64_t k = 0;; k += 3) {
-      if (k + 2 < nb) load(c, k + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      use(a, k);
-      if (k + 1 >= nb) return;
-      if (k + 3 < nb) load(a, k + 3);
-      __builtin_amdgcn_sched_barrier(0);
-      use(b, k + 1);
-      if (k + 2 >= nb) return;
-      if (k + 4 < nb) load(b, k + 4);
-      __builtin_amdgcn_sched_barrier(0);
-      use(c, k + 2);
-      if (k + 3 >= nb) return;
-    }
-  }
-}
-
 // Memory ordering without a device-scope fence (an agent-scope release writes the whole L2 back
 // and serialised a first version: 0.25-0.35 us per workgroup, profiles/r03b_tune_stats_fence.log):
 // partials are written with agent-coherent (sc1) stores, every thread waits for its own stores
@@ -462,10 +372,7 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
       acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
     }
   };
-  if (QZ_STATS_WALK && (int64_t)QZ_ABS1_NB * S * ld < (1LL << 30))
-    stats_walk_u<S, QZ_ABS1_NB, QZ_STATS_DIST>(x, c0, ld, t0 + wv * RPW, q, t1, row);
-  else
-    stats_walk<S, QZ_ABS1_NB, QZ_ABS1_PP>(x + c0, ld, t0 + wv * RPW, q, t1, row);
+  stats_walk<S, QZ_ABS1_NB, QZ_ABS1_PP>(x + c0, ld, t0 + wv * RPW, q, t1, row);
   stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum);
 }
 
@@ -488,51 +395,22 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
   const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
-#ifndef QZ_WM_PROBE
-#define QZ_WM_PROBE 0  // speed-of-light probes (NOT the w_mean arithmetic): 1 f32 sums, 2 no group max, 3 |w| only
-#endif
-#if QZ_WM_PROBE == 1 || QZ_WM_PROBE == 3
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#else
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
   auto row = [&](const uint4 v, bool ok) {
     const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
-#if QZ_WM_PROBE == 3
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      acc[2 * k] += __uint_as_float(u[k] << 16);
-      acc[2 * k + 1] += __uint_as_float(u[k] & 0xffff0000u);
-    }
-    return;
-#endif
     // group absmax on |bf16| bit patterns (v_pk_max_u16 + DPP, every lane of the group on the same
     // row, so the group is uniformly valid or not), then |w| / bf16(amax + 1e-6)
     const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
     const float m = __uint_as_float(grp_max_u<L>(max(pm & 0xffffu, pm >> 16)) << 16);
-#if QZ_WM_PROBE == 2
-    const float rd = ok ? 1.0f : 0.f;
-#else
     const float rd = ok ? __builtin_amdgcn_rcpf(bfr1(m + 1e-6f)) : 0.f;  // rcp lemma; 0: adds +0.0
-#endif
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       acc[2 * k] += (double)bfr1(__uint_as_float(u[k] << 16) * rd);
       acc[2 * k + 1] += (double)bfr1(__uint_as_float(u[k] & 0xffff0000u) * rd);
     }
   };
-  if (QZ_STATS_WALK && (int64_t)QZ_WM1_NB * S * ld < (1LL << 30))
-    stats_walk_u<S, QZ_WM1_NB, QZ_STATS_DIST>(w, c0, ld, r0 + wv * RPW, q, r1, row);
-  else
-    stats_walk<S, QZ_WM1_NB, QZ_WM1_PP>(w + c0, ld, r0 + wv * RPW, q, r1, row);
-#if QZ_WM_PROBE == 1 || QZ_WM_PROBE == 3
-  double accd[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) accd[i] = acc[i];
-  stats_finish<WIN, SWP>(red, accd, lane, wv, C, nch, cpg, part, gpart, cnt, wsum);
-#else
+  stats_walk<S, QZ_WM1_NB, QZ_WM1_PP>(w + c0, ld, r0 + wv * RPW, q, r1, row);
   stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum);
-#endif
 }
 
 // ------------------------------------- a3 / a4, one launch, LDS-DMA walk (round 4)

@@ -473,15 +473,7 @@ __device__ __forceinline__ void process_tile(const FastArgs& A, const QP& p, con
     const int64_t local = tile * (UNROLL * WAVE) + u * WAVE + lane;
     const int64_t unit = b * A.units_per_batch + local;
     const bool valid = local < A.units_per_batch;
-#ifdef QZ_TUNE_NULL_COMPUTE  // tuning probe only: same traffic, no arithmetic
-    const uint32_t h = v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
-    if (valid) {
-      reinterpret_cast<uint32_t*>(A.q_out)[unit] = h;
-      if ((lane & 15) == 0) reinterpret_cast<uint16_t*>(A.s_out)[unit >> 4] = (uint16_t)v[u].x;
-    }
-#else
     process_unit<LOGL, KIND, FQ, SYM, NTS>(A, p, v[u], unit, valid, gs, lane, b, csu[u]);
-#endif
   }
 }
 
