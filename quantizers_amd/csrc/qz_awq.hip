@@ -425,7 +425,7 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
 // row r0 + w, r0 + w + S, ... for wave w), the ring memory reused for stats_finish's reduction:
 // the same fixed-order tree as the kernels above with WIN = 512, RPW = 1, TF = 1.
 #ifndef QZ_STATS_DMA
-#define QZ_STATS_DMA 1  // 1: the LDS-DMA walk for aligned absmean / w_mean; 0: k_absmean_1l / k_wmean_1l (A/B)
+#define QZ_STATS_DMA 0  // 1: the LDS-DMA walk for aligned absmean / w_mean; 0: k_absmean_1l / k_wmean_1l (A/B)
 #endif
 #ifndef QZ_DMA_D
 #define QZ_DMA_D 8  // ring slots (KiB in flight) per wave

@@ -787,3 +787,41 @@ def test_whole_model_plan_equals_per_weight(cuda):
     assert len(seen) == 5
     del model, plan, got
     torch.cuda.empty_cache()
+
+
+def test_stats_one_launch_stress_many_grids(cuda):
+    """the one-launch statistics reductions hand partials between workgroups through
+    agent-coherent stores / loads and counters (no release / acquire fence).  Over 24 grid shapes
+    (1 to 64 chunks per window, ragged windows, both statistics), each call repeated while a GEMM
+    stream loads the card, every result equals the restated fixed-order tree bit for bit and the
+    counters are left zero."""
+    import numpy as np
+    rng = np.random.default_rng(7)
+    side = torch.cuda.Stream()
+    junk = torch.randn(2048, 2048, device=cuda)
+    for case in range(24):
+        which = "absmean" if case % 2 == 0 else "wmean"
+        cols = int(rng.choice([264, 520, 1032, 2048, 2560, 4096]))
+        g = int(rng.choice([32, 64, 128])) if which == "wmean" else 0
+        cols -= cols % max(g, 8)
+        rows = int(rng.integers(8, 9000))
+        x = _w(rows, cols, seed=1000 + case, scale=0.02 if which == "wmean" else 1.0)
+        xd = x.to(cuda)
+        if which == "absmean":
+            lay = ops.awq_stats_layout("absmean", rows, cols)
+            want = torch.from_numpy(_stats_tree(x.float().abs().numpy(), lay, np.float32))
+        else:
+            want = _wmean_tree(x, g)
+        for rep in range(3):
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    junk = junk @ junk.T / 2048
+            out = torch.zeros(cols, dtype=torch.float32 if which == "absmean" else torch.float64, device=cuda)
+            if which == "absmean":
+                ops.awq_absmean_accum(xd, out)
+            else:
+                ops.awq_weight_mean_accum(xd, g, out)
+            torch.cuda.synchronize()
+            assert torch.equal(out.cpu(), want), (case, which, rows, cols, g, rep)
+    for buf in ops._stats_ws_cache.values():
+        assert not buf[:32768].any()
