@@ -1111,14 +1111,15 @@ struct NvArgs {
   QP p;
 };
 
-// the current value of a sync word, read AT THE MEMORY SIDE: a compare-exchange that always fails
-// (no sync word ever holds 0xffffffff).  A relaxed agent-scope atomic load, or an idempotent RMW
-// (which LLVM turns into one), compiles to a global_load ... sc1 that can be served from this
-// XCD's L2 copy of the line while another XCD's atomics update it (per-XCD L2s are not coherent).
-__device__ __forceinline__ uint32_t sync_read(uint32_t* p) {
-  uint32_t e = 0xffffffffu;
-  __hip_atomic_compare_exchange_strong(p, &e, 0xfffffffeu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+// Sync words are read AT THE MEMORY SIDE, by a compare-exchange that always fails (no sync pair
+// ever holds all ones): a relaxed agent-scope atomic load, or an idempotent RMW (which LLVM turns
+// into one), compiles to a global_load ... sc1 that can be served from this XCD's L2 copy of the
+// line while other XCDs' atomics update it (per-XCD L2s are not coherent).
+// the 8-byte {key, count} pair of a slice, both words in ONE memory-side round trip
+__device__ __forceinline__ uint64_t sync_read2(uint32_t* p) {
+  uint64_t e = ~0ull;
+  __hip_atomic_compare_exchange_strong(reinterpret_cast<uint64_t*>(p), &e, ~0ull - 1, __ATOMIC_RELAXED,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return e;
 }
 constexpr int NV_SYNC_STRIDE = 16;  // uint32 words per slice: one 64-B line each
@@ -1188,16 +1189,19 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
       const uint32_t old = __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       uint32_t cnt = __hip_atomic_fetch_add(sy + 1, 1u + (old >> 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
       uint32_t timed_out = 0;
+      // {key, count} polled together: once the count reaches n, the key read in the same atomic
+      // snapshot is final (every arrival's max was performed before its count add)
+      uint64_t kc = cnt < n ? 0ull : sync_read2(sy);
       if (cnt < n) {
         const uint64_t t0 = wall_clock64();
         for (;;) {
           __builtin_amdgcn_s_sleep(2);
-          cnt = sync_read(sy + 1);
-          if (cnt >= n) break;
+          kc = sync_read2(sy);
+          if ((uint32_t)(kc >> 32) >= n) break;
           if (wall_clock64() - t0 > A.spin_ticks) { timed_out = 1; break; }
         }
       }
-      bc[0] = timed_out ? 0u : sync_read(sy);
+      bc[0] = timed_out ? 0u : (uint32_t)kc;
       bc[1] = timed_out;
     }
     __syncthreads();

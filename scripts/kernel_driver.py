@@ -40,6 +40,28 @@ def main(n=30):
         ("weight_mean", lambda i: ops.awq_weight_mean_accum(copies[i % 12], G, wsum), 1),
         ("scale_columns", lambda i: ops.scale_columns_(copies[i % 12], s), 1),
     ]
+    # NVFP4 (the reference's Qwen3-30B-A3B recipe): one fused expert half [128, 768, 2048] per
+    # launch (strided slices of [128, 1536, 2048]), 4 resident parameters rotated (1.6 GB)
+    nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16,
+                          scale_dtype="float8_e4m3fn")
+    gus = [(torch.randn(128, 1536, 2048, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for _ in range(4)]
+    nv_out = ops.alloc_outputs((128, 768, 2048), nv, None, dev)
+    import ctypes
+    from quantizers_amd import _lib
+    lib, ca = _lib.load(), nv.to_c()
+    nv_ws = torch.empty(lib.qz_quantize_workspace_size(128, 768, 2048, ctypes.byref(ca)) + 256, dtype=torch.uint8,
+                        device=dev)
+
+    def nv_two_pass(i):
+        w = gus[i % 4][:, :768]
+        rc = lib.qz_quantize(ops._ptr(w), 128, 768, 2048, 2048, 1536 * 2048, ctypes.byref(ca), _lib.QZ_OUT_FP4_PACKED,
+                             ops._ptr(nv_out["codes"]), ops._ptr(nv_out["scale"]), ops._ptr(None),
+                             ops._ptr(nv_out["global_scale"]), ops._ptr(nv_ws), nv_ws.numel(), ops._stream())
+        _lib.check(rc, "qz_quantize")
+    kernels += [
+        ("nvfp4_single_read", lambda i: ops.quantize_weight(gus[i % 4][:, :768], nv, out=nv_out), 1),
+        ("nvfp4_two_pass", nv_two_pass, 1),
+    ]
     st = torch.cuda.current_stream()
     for name, fn, _ in kernels:
         for i in range(3):
