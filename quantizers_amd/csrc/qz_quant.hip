@@ -1085,14 +1085,17 @@ __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_
 // counter, so the sync region is zero after every call (caller contract: zero before the
 // first call).
 #ifndef QZ_NV_PIPE
-#define QZ_NV_PIPE 1  // 1: the next item's loads are in flight while the current item waits (A/B knob)
+#define QZ_NV_PIPE 1  // 1: slices that fit take the pipelined instantiation (A/B knob; 0: the held-only one)
 #endif
-#ifndef QZ_NV_U
-#define QZ_NV_U (QZ_NV_PIPE ? 8 : 16)
-#endif
-constexpr int NV_U = QZ_NV_U;  // 16-B units per lane per item (x2 with the pipeline: 64 VGPRs)
+// Two instantiations: PIPE (8 units per lane per item, 32 KiB, the next item's loads in flight
+// while the current one waits: 2 x 32 VGPRs) for slices of up to `capacity` items, and the
+// held-only one (16 units per lane, 64 KiB per item, 64 VGPRs) for slices up to twice that
+// (dense NVFP4 linears such as Qwen3-4B's [9728, 2560] gate / up).
+template <bool PIPE>
+constexpr int nv_units() { return PIPE ? 8 : 16; }
 constexpr int NV_BLOCK = 256;
-constexpr int64_t NV_CHUNK = (int64_t)NV_BLOCK * NV_U;  // units per item (64 KiB of bf16 at U = 16)
+template <bool PIPE>
+constexpr int64_t nv_chunk() { return (int64_t)NV_BLOCK * nv_units<PIPE>(); }  // units per item
 
 struct NvArgs {
   const uint64_t* tab;  // table mode: DEVICE [4][n_slices] {weight, codes, scales, global scale}; null = batch mode
@@ -1128,8 +1131,10 @@ __device__ __forceinline__ uint32_t absmax_bits(const uint4 v) {
   return pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu), pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu));
 }
 
-template <bool TAB>
+template <bool TAB, bool PIPE>
 __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
+  constexpr int NV_U = nv_units<PIPE>();
+  constexpr int64_t NV_CHUNK = nv_chunk<PIPE>();
   __shared__ uint32_t red[NV_BLOCK / WAVE];
   __shared__ uint32_t bc[2];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid >> 6;
@@ -1156,7 +1161,7 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
     const int64_t base = (item - b * A.items_per_slice) * NV_CHUNK;
     const int64_t next = item + gridDim.x;
     uint4 nv[NV_U];
-    if (QZ_NV_PIPE && next < A.n_items) load(nv, next);  // in flight while this item waits
+    if (PIPE && next < A.n_items) load(nv, next);  // in flight while this item waits
     FastArgs F;
     const uint4* src;
     float* gs_out;
@@ -1233,7 +1238,7 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
       }
     }
     if (next < A.n_items) {
-      if constexpr (QZ_NV_PIPE) {
+      if constexpr (PIPE) {
 #pragma unroll
         for (int u = 0; u < NV_U; ++u) v[u] = nv[u];
       } else {
@@ -1591,22 +1596,27 @@ WS ws_layout(void* base, int64_t batch, const Plan& pl) {
 size_t ws_size(int64_t batch, const Plan& pl) { return ws_layout(nullptr, batch, pl).bytes; }
 
 // resident 256-thread k_nv_hold workgroups on the current device (occupancy query x CUs, at most
-// 8 per CU: MI355X_MICROARCH.md "Residency"), cached per device
-int64_t nv_capacity(bool tab) {
+// 8 per CU: MI355X_MICROARCH.md "Residency"), per instantiation, cached per device
+template <bool TAB, bool PIPE>
+int64_t nv_capacity_of(int dev) {
   static std::mutex mu;
-  static int64_t cap[2][64] = {};
+  static int64_t cap[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (cap[dev] == 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<TAB, PIPE>, NV_BLOCK, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
+        cus <= 0)
+      return 0;
+    cap[dev] = (int64_t)std::min(per_cu, 8) * cus;
+  }
+  return cap[dev];
+}
+int64_t nv_capacity(bool tab, bool pipe) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  std::lock_guard<std::mutex> lk(mu);
-  if (cap[tab][dev] == 0) {
-    int per_cu = 0, cus = 0;
-    const hipError_t e1 = tab ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<true>, NV_BLOCK, 0)
-                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<false>, NV_BLOCK, 0);
-    const hipError_t e2 = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e1 != hipSuccess || e2 != hipSuccess || per_cu <= 0 || cus <= 0) return 0;
-    cap[tab][dev] = (int64_t)std::min(per_cu, 8) * cus;
-  }
-  return cap[tab][dev];
+  if (tab) return pipe ? nv_capacity_of<true, true>(dev) : nv_capacity_of<true, false>(dev);
+  return pipe ? nv_capacity_of<false, true>(dev) : nv_capacity_of<false, false>(dev);
 }
 
 // the bounded wait of k_nv_hold in 100 MHz ticks (default 1 ms); QZ_NV_SPIN_TICKS is a test knob
@@ -1633,17 +1643,28 @@ int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st
   if (!sync) return QZ_ERR_NULL;
   if (!aligned(sync, 16)) return QZ_ERR_ALIGN;
   if (sync_bytes < NV_SYNC_HEAD + 4 * NV_SYNC_STRIDE * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
-  const int64_t cap = nv_capacity(tab);
+  // the pipelined instantiation when the slice fits its capacity, else the held-only one
+  bool pipe = QZ_NV_PIPE != 0;
+  int64_t cap = nv_capacity(tab, pipe);
+  if (pipe && cdiv(A.units_per_slice, nv_chunk<true>()) > cap) {
+    pipe = false;
+    cap = nv_capacity(tab, false);
+  }
   if (cap <= 0) return (int)hipErrorInvalidDevice;
-  A.items_per_slice = cdiv(A.units_per_slice, NV_CHUNK);
+  A.items_per_slice = cdiv(A.units_per_slice, pipe ? nv_chunk<true>() : nv_chunk<false>());
   if (A.items_per_slice > cap) return QZ_ERR_CAPACITY;
   A.n_items = A.n_slices * A.items_per_slice;
   A.diag = (uint32_t*)sync;
   A.sync = (uint32_t*)((char*)sync + NV_SYNC_HEAD);
   A.spin_ticks = nv_spin_ticks();
   const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, cap);
-  if (tab) hipLaunchKernelGGL(k_nv_hold<true>, dim3(grid), dim3(NV_BLOCK), 0, st, A);
-  else hipLaunchKernelGGL(k_nv_hold<false>, dim3(grid), dim3(NV_BLOCK), 0, st, A);
+  if (tab) {
+    if (pipe) hipLaunchKernelGGL((k_nv_hold<true, true>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
+    else hipLaunchKernelGGL((k_nv_hold<true, false>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
+  } else {
+    if (pipe) hipLaunchKernelGGL((k_nv_hold<false, true>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
+    else hipLaunchKernelGGL((k_nv_hold<false, false>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
+  }
   return launch_err();
 }
 
@@ -1998,10 +2019,10 @@ size_t qz_nvfp4_sync_size(int64_t n_slices) {
 
 int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols) {
   if (rows <= 0 || cols <= 0 || cols % 16) return -1;
-  return cdiv(rows * cols / 8, NV_CHUNK);
+  return cdiv(rows * cols / 8, nv_chunk<true>());
 }
 
-int64_t qz_nvfp4_capacity(void) { return nv_capacity(false); }
+int64_t qz_nvfp4_capacity(void) { return nv_capacity(false, true); }
 
 int qz_quantize_nvfp4(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_batch, const qz_args* a,
                       void* q_out, void* scale_out, float* gscale_out, void* sync, size_t sync_bytes,
