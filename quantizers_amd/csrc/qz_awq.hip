@@ -17,6 +17,7 @@ using namespace qz;
 namespace {
 
 constexpr int WAVE = 64;
+typedef uint32_t qz_u32x4 __attribute__((ext_vector_type(4)));
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 __device__ __forceinline__ int64_t cdiv_d(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -212,12 +213,20 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 // register sets used in turn (no copies between them, but the loop body twice: more VGPRs --
 // taken by w_mean, whose grid is 2 waves per SIMD anyway); otherwise the next batch is copied
 // into the current one (absmean: 8 waves per SIMD need the VGPRs).
+#ifndef QZ_STATS_NT
+#define QZ_STATS_NT 0  // 1: non-temporal 16-B loads in the one-launch statistics walk (A/B knob)
+#endif
 template <int S, int SNB, bool PP, typename F>
 __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int64_t rb, int q, int64_t r1, F&& f) {
   if (rb >= r1) return;
   const uint32_t rlast = (uint32_t)(r1 - 1), uld = (uint32_t)ld;
   auto ld16 = [&](int64_t r) {
-    return *reinterpret_cast<const uint4*>(base + (uint64_t)std::min((uint32_t)r, rlast) * uld);
+    const uint4* p = reinterpret_cast<const uint4*>(base + (uint64_t)std::min((uint32_t)r, rlast) * uld);
+    if constexpr (QZ_STATS_NT) {
+      return __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const qz_u32x4*>(p)));
+    } else {
+      return *p;
+    }
   };
   constexpr int64_t STEP = (int64_t)SNB * S;
   uint4 a[SNB], b[SNB];
@@ -438,7 +447,6 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
 #endif
 constexpr int DMA_NW = 8, DMA_D = QZ_DMA_D, DMA_WIN = 512;
 
-typedef uint32_t qz_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 lds_read16(const void* p) {
   const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
   qz_u32x4 t;

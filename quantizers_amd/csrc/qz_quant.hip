@@ -1091,8 +1091,11 @@ __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_
 // while the current one waits: 2 x 32 VGPRs) for slices of up to `capacity` items, and the
 // held-only one (16 units per lane, 64 KiB per item, 64 VGPRs) for slices up to twice that
 // (dense NVFP4 linears such as Qwen3-4B's [9728, 2560] gate / up).
+#ifndef QZ_NV_PIPE_U
+#define QZ_NV_PIPE_U 8  // units per lane per item of the pipelined instantiation (3 buffers)
+#endif
 template <bool PIPE>
-constexpr int nv_units() { return PIPE ? 8 : 16; }
+constexpr int nv_units() { return PIPE ? QZ_NV_PIPE_U : 16; }
 constexpr int NV_BLOCK = 256;
 template <bool PIPE>
 constexpr int64_t nv_chunk() { return (int64_t)NV_BLOCK * nv_units<PIPE>(); }  // units per item
@@ -1131,73 +1134,65 @@ __device__ __forceinline__ uint32_t absmax_bits(const uint4 v) {
   return pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu), pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu));
 }
 
+#ifndef QZ_NV_PIPE_WAVES
+#define QZ_NV_PIPE_WAVES 3  // minimum waves per SIMD of the pipelined instantiation (VGPR budget)
+#endif
+// held-only: 64 data VGPRs + the encode's; 4 waves per SIMD spills (128-VGPR cap), so 3
 template <bool TAB, bool PIPE>
-__global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
+__global__ __launch_bounds__(NV_BLOCK, PIPE ? QZ_NV_PIPE_WAVES : 3) void k_nv_hold(NvArgs A) {
   constexpr int NV_U = nv_units<PIPE>();
   constexpr int64_t NV_CHUNK = nv_chunk<PIPE>();
-  __shared__ uint32_t red[NV_BLOCK / WAVE];
+  __shared__ uint32_t red[2][NV_BLOCK / WAVE];  // alternating: arrival k + 2 reuses arrival k's slots
   __shared__ uint32_t bc[2];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid >> 6;
   QP p = A.p;
   p.kind = K_NV;
   p.sym = 1;
-  const int64_t ups = A.units_per_slice;
+  const int64_t ups = A.units_per_slice, G = gridDim.x, N = A.n_items;
   const uint32_t n = (uint32_t)A.items_per_slice;
+  auto slice_src = [&](int64_t bb) {
+    return TAB ? reinterpret_cast<const uint4*>(A.tab[bb]) : reinterpret_cast<const uint4*>(A.w + bb * A.ld_batch);
+  };
   auto load = [&](uint4 (&v)[NV_U], int64_t it) {  // out-of-range lanes re-read the slice's last unit
     const int64_t bb = it / A.items_per_slice;
     const int64_t b0 = (it - bb * A.items_per_slice) * NV_CHUNK;
-    const uint4* s0 = TAB ? reinterpret_cast<const uint4*>(A.tab[bb]) : reinterpret_cast<const uint4*>(A.w + bb * A.ld_batch);
+    const uint4* s0 = slice_src(bb);
 #pragma unroll
     for (int u = 0; u < NV_U; ++u) {
       const int64_t un = min<int64_t>(b0 + u * NV_BLOCK + tid, ups - 1);
       v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + un)));
     }
   };
-  if ((int64_t)blockIdx.x >= A.n_items) return;
-  uint4 v[NV_U];
-  load(v, blockIdx.x);
-  for (int64_t item = blockIdx.x; item < A.n_items; item += gridDim.x) {
-    const int64_t b = item / A.items_per_slice;
-    const int64_t base = (item - b * A.items_per_slice) * NV_CHUNK;
-    const int64_t next = item + gridDim.x;
-    uint4 nv[NV_U];
-    if (PIPE && next < A.n_items) load(nv, next);  // in flight while this item waits
-    FastArgs F;
-    const uint4* src;
-    float* gs_out;
-    if constexpr (TAB) {
-      src = reinterpret_cast<const uint4*>(A.tab[b]);
-      F.q_out = reinterpret_cast<void*>(A.tab[A.n_slices + b]);
-      F.s_out = reinterpret_cast<void*>(A.tab[2 * A.n_slices + b]);
-      gs_out = reinterpret_cast<float*>(A.tab[3 * A.n_slices + b]);
-    } else {
-      src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
-      F.q_out = reinterpret_cast<uint32_t*>(A.q_out) + b * ups;
-      F.s_out = reinterpret_cast<uint8_t*>(A.s_out) + b * (ups >> 1);
-      gs_out = A.gs_out + b;
-    }
-    F.zp_out = nullptr;
-    F.scale_bytes = 1;
-    F.out_fmt = QZ_OUT_FP4_PACKED;
-    F.col_scales = nullptr;
+  int parity = 0;
+  // arrival: the item's |bf16| maximum over the workgroup, then (one lane) an agent-scope max into
+  // the slice's key and an add to its count -- the add depends on the max's RETURNED value (whose
+  // top bit is never set), so the max has been performed at the memory side before it counts
+  auto arrive = [&](const uint4 (&v)[NV_U], int64_t it) {
     uint32_t m = 0;
 #pragma unroll
     for (int u = 0; u < NV_U; ++u) m = pk_max_u16(m, absmax_bits(v[u]));
     m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
-    if (lane == 0) red[wv] = m;
+    if (lane == 0) red[parity][wv] = m;
     __syncthreads();
+    if (tid == 0) {
+      m = max(max(red[parity][0], red[parity][1]), max(red[parity][2], red[parity][3]));
+      uint32_t* sy = A.sync + NV_SYNC_STRIDE * (it / A.items_per_slice);
+      const uint32_t old = __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(sy + 1, 1u + (old >> 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    parity ^= 1;
+  };
+  // completion: wait until every item of the slice has arrived ({key, count} polled together in
+  // one memory-side CAS: once the count reaches n the key of the same snapshot is final), encode
+  // and store the held units, depart (the slice's last leaver resets its sync words)
+  auto finish = [&](const uint4 (&v)[NV_U], int64_t it) {
+    const int64_t b = it / A.items_per_slice;
+    const int64_t base = (it - b * A.items_per_slice) * NV_CHUNK;
     uint32_t* sy = A.sync + NV_SYNC_STRIDE * b;
     if (tid == 0) {
-      m = max(max(red[0], red[1]), max(red[2], red[3]));
-      // the arrival add depends on the max's RETURNED value (its top bit is never set): the max
-      // has been performed at the memory side before this workgroup counts as arrived
-      const uint32_t old = __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t cnt = __hip_atomic_fetch_add(sy + 1, 1u + (old >> 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
       uint32_t timed_out = 0;
-      // {key, count} polled together: once the count reaches n, the key read in the same atomic
-      // snapshot is final (every arrival's max was performed before its count add)
-      uint64_t kc = cnt < n ? 0ull : sync_read2(sy);
-      if (cnt < n) {
+      uint64_t kc = sync_read2(sy);
+      if ((uint32_t)(kc >> 32) < n) {
         const uint64_t t0 = wall_clock64();
         for (;;) {
           __builtin_amdgcn_s_sleep(2);
@@ -1211,39 +1206,80 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_hold(NvArgs A) {
     }
     __syncthreads();
     uint32_t key = bc[0];
+    const uint4* src = slice_src(b);
     if (bc[1]) {  // bounded wait expired: the slice's maximum from the slice itself (exact, slow)
       uint32_t mm = 0;
       for (int64_t un = tid; un < ups; un += NV_BLOCK) mm = pk_max_u16(mm, absmax_bits(src[un]));
       mm = grp_max_u<WAVE>(max(mm & 0xffffu, mm >> 16));
-      if (lane == 0) red[wv] = mm;
+      if (lane == 0) red[parity][wv] = mm;
       __syncthreads();
-      key = max(max(red[0], red[1]), max(red[2], red[3]));
+      key = max(max(red[parity][0], red[parity][1]), max(red[parity][2], red[parity][3]));
       if (tid == 0) __hip_atomic_fetch_add(A.diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
     }
+    FastArgs F;
+    float* gs_out;
+    if constexpr (TAB) {
+      F.q_out = reinterpret_cast<void*>(A.tab[A.n_slices + b]);
+      F.s_out = reinterpret_cast<void*>(A.tab[2 * A.n_slices + b]);
+      gs_out = reinterpret_cast<float*>(A.tab[3 * A.n_slices + b]);
+    } else {
+      F.q_out = reinterpret_cast<uint32_t*>(A.q_out) + b * ups;
+      F.s_out = reinterpret_cast<uint8_t*>(A.s_out) + b * (ups >> 1);
+      gs_out = A.gs_out + b;
+    }
+    F.zp_out = nullptr;
+    F.scale_bytes = 1;
+    F.out_fmt = QZ_OUT_FP4_PACKED;
+    F.col_scales = nullptr;
     // global scale, k_gscale_keys' arithmetic: bf16(bf16(1 / absmax) * (448 * 6))
-    const float am = __uint_as_float(key << 16);
-    const float gs = bfr(bfr(1.0f / am) * 2688.0f);
+    const float gs = bfr(bfr(1.0f / __uint_as_float(key << 16)) * 2688.0f);
     if (base == 0 && tid == 0) *gs_out = gs;
 #pragma unroll
     for (int u = 0; u < NV_U; ++u) {
       const int64_t local = base + u * NV_BLOCK + tid;
       process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
     }
-    if (tid == 0) {  // depart; the slice's last leaver resets its sync words for the next call
+    if (tid == 0) {
       const uint32_t old = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (old == 2u * n - 1u) {
         __hip_atomic_store(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sy + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    if (next < A.n_items) {
-      if constexpr (PIPE) {
+  };
+  int64_t ia = blockIdx.x;
+  if (ia >= N) return;
+  if constexpr (!PIPE) {  // one held item at a time
+    uint4 v[NV_U];
+    for (; ia < N; ia += G) {
+      load(v, ia);
+      arrive(v, ia);
+      finish(v, ia);
+    }
+  } else {
+    // two ARRIVED items held (a: the oldest, b) and one in flight (c): item k + 2 arrives only
+    // after item k is finished, so a slice's wait overlaps the next item's
+    uint4 va[NV_U], vb[NV_U], vc[NV_U];
+    int64_t ib = ia + G, ic = ib + G;
+    load(va, ia);
+    if (ib < N) load(vb, ib);
+    arrive(va, ia);
+    if (ib < N) arrive(vb, ib);
+    if (ic < N) load(vc, ic);
+    for (;;) {
+      finish(va, ia);
+      if (ib >= N) break;
+      ia = ib;
 #pragma unroll
-        for (int u = 0; u < NV_U; ++u) v[u] = nv[u];
-      } else {
-        load(v, next);
-      }
+      for (int u = 0; u < NV_U; ++u) va[u] = vb[u];
+      ib = ic;
+      if (ib >= N) continue;  // one arrived item left
+#pragma unroll
+      for (int u = 0; u < NV_U; ++u) vb[u] = vc[u];
+      ic += G;
+      arrive(vb, ib);
+      if (ic < N) load(vc, ic);
     }
   }
 }
