@@ -206,10 +206,13 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
     """The reference's own Qwen3-30B-A3B recipe (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21
     -> NVFP4: E2M1 codes, e4m3 group-16 scales, one f32 global scale per expert linear): every
     expert weight of the 48 layers (4 resident fused layers rotated, as the MXFP4 leg) through
-    the single-read kernel (qz_quantize_nvfp4 -> k_nv_hold, one launch per fused parameter),
-    outputs preallocated.  HIP events on the launch stream around one whole pass (144 launches
-    back to back); the two-pass qz_quantize path timed the same way beside it.  Algorithmic bytes
-    per param = 2.5625 (+ 4 B per expert linear)."""
+    the fused NVFP4 path (qz_quantize_nvfp4 -> k_nv_absmax + k_nv_encode, two launches per fused
+    parameter, no fills), outputs preallocated.  HIP events on the launch stream around one whole
+    pass (288 launches back to back); the generic qz_quantize path (absmax pre-pass, global-scale
+    launch, group kernel: five launches) timed the same way beside it.  Algorithmic bytes per
+    param = 2.5625 (+ 4 B per expert linear); the path reads every weight twice (the global
+    scale needs the whole slice first), so ``streamed_frac`` also prices the
+    second read (4.5625 B per param)."""
     import ctypes
     from quantizers_amd import _lib
     nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16,
@@ -221,7 +224,7 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
     ws = torch.empty(lib.qz_quantize_workspace_size(128, 2048, 768, ctypes.byref(ca)) + 256, dtype=torch.uint8,
                      device=dev)
 
-    def single():
+    def fused():
         for li in range(48):
             for lj, j, w in views[(li % 4) * 3:(li % 4) * 3 + 3]:
                 ops.quantize_weight(w, nv, out=outs[(lj, j)])
@@ -237,11 +240,11 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
                 _lib.check(rc, "qz_quantize")
     npar = 48 * 128 * 3 * 768 * 2048
     nb = npar * NV_B_PER_PARAM + 48 * 3 * 128 * 4
-    res = {"params": npar, "alg_bytes": nb, "kernel": "k_nv_hold<false> (qz_quantize_nvfp4)",
+    res = {"params": npar, "alg_bytes": nb, "kernel": "k_nv_absmax<false> + k_nv_encode<false> (qz_quantize_nvfp4)",
            "recipe": "reference configs/recipes/recipe_MoE_RTN_NVFP4.yaml (scheme NVFP4)",
-           "timing": "HIP events around one whole pass (144 launches back to back), best of 3"}
+           "timing": "HIP events around one whole pass (144 fused parameters back to back), best of 3"}
     st = torch.cuda.current_stream(dev)
-    for name, fn in (("single_read", single), ("two_pass", two_pass)):
+    for name, fn in (("fused", fused), ("two_pass", two_pass)):
         fn()
         torch.cuda.synchronize()
         best = None
@@ -254,10 +257,10 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
             best = e0.elapsed_time(e1) * 1e-3 if best is None else min(best, e0.elapsed_time(e1) * 1e-3)
         gbps = nb / best / 1e9
         leg = {"ms": best * 1e3, "params_per_s": npar / best, "alg_GBps": gbps, "frac": gbps / HBM_PEAK_GBS,
-               "read_frac": npar * 2 / best / 1e9 / HBM_PEAK_GBS}
-        if name == "single_read":
+               "read_frac": npar * 2 / best / 1e9 / HBM_PEAK_GBS,
+               "streamed_frac": (npar * (NV_B_PER_PARAM + 2) + 48 * 3 * 128 * 4) / best / 1e9 / HBM_PEAK_GBS}
+        if name == "fused":
             res.update(leg)
-            res["bounded_wait_timeouts"] = ops.nvfp4_timeouts(dev)
         else:
             res["two_pass_qz_quantize"] = leg
     del outs

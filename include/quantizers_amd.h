@@ -78,8 +78,7 @@ enum {
   QZ_ERR_FORMAT = -7,       /* output format incompatible with args */
   QZ_ERR_WORKSPACE = -8,    /* workspace smaller than qz_quantize_workspace_size() */
   QZ_ERR_ALIGN = -9,        /* pointer/ld alignment violated where required */
-  QZ_ERR_UNAVAILABLE = -10, /* a runtime dependency is not loaded / refused the call (qz_expert_gemms: hipBLASLt) */
-  QZ_ERR_CAPACITY = -11     /* NVFP4 single-read path: a slice needs more workgroups than are resident at once */
+  QZ_ERR_UNAVAILABLE = -10  /* a runtime dependency is not loaded / refused the call (qz_expert_gemms: hipBLASLt) */
 };
 
 const char* qz_strerror(int code);
@@ -159,29 +158,24 @@ int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* row
 
 /*
  * qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4 -- NVFP4 (TENSOR_GROUP, FP4 E2M1, group 16, e4m3
- * group scales, f32 per-slice global scale) in ONE read of the weight.  Replaces the same
- * observer -> calculate_qparams -> quantize -> pack_fp4_to_uint8 chain as qz_quantize for the
+ * group scales, f32 per-slice global scale) in TWO launches and no workspace fills.  Replaces the
+ * same observer -> calculate_qparams -> quantize -> pack_fp4_to_uint8 chain as qz_quantize for the
  * reference's NVFP4 recipes (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21,
  * recipe_Dense_NVFP4.yaml:7-12; scheme preset NVFP4), with results identical to qz_quantize's.
- * qz_quantize reads each slice twice (its global scale needs the whole slice's |w| maximum
- * first); here a persistent grid holds every slice's chunks in registers until the slice's
- * maximum is known.
+ * The first launch reduces every slice's |w| maximum into `sync`, the second encodes (each slice
+ * is read twice: its global scale needs the whole slice first).
  *   qz_quantize_nvfp4: a batch of dense-row slices, slice b at w + b * ld_batch (ld_batch % 8 == 0,
  *     w 16-B aligned); outputs as qz_quantize's (codes uint8 [batch][rows][cols/2], scales e4m3
  *     [batch][rows][cols/16], gscale f32 [batch]).
- *   qz_quantize_grouped_nvfp4: n independent dense [rows, cols] weights, DEVICE table of 4*n
- *     uint64 {weights, codes, scales, global-scale pointers} (qz_quantize_grouped's layout with
- *     the zero-point row replaced by each weight's f32 global scale).
+ *   qz_quantize_grouped_nvfp4: n independent dense [rows, cols] weights of one shape in the same
+ *     two launches, DEVICE table of 4*n uint64 {weights, codes, scales, global-scale pointers}
+ *     (qz_quantize_grouped's layout with the zero-point row replaced by each weight's f32 global
+ *     scale).
  * `sync`: caller-owned DEVICE region of qz_nvfp4_sync_size(slices) bytes, 16-B aligned, ZERO
  * before its first use; every call leaves it zero.  Do not share one region between calls that
- * may run concurrently (e.g. on two streams).  sync[0] (uint32) counts bounded waits that timed
- * out (another kernel held CUs): the results are exact either way, only slower.
- * QZ_ERR_CAPACITY: one slice needs more than qz_nvfp4_capacity() workgroups
- * (qz_nvfp4_items_per_slice(rows, cols) of 64 KiB); use qz_quantize.
+ * may run concurrently (e.g. on two streams).
  */
 size_t qz_nvfp4_sync_size(int64_t n_slices);
-int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols);
-int64_t qz_nvfp4_capacity(void);
 int qz_quantize_nvfp4(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_batch, const qz_args* a,
                       void* q_out, void* scale_out, float* gscale_out, void* sync, size_t sync_bytes,
                       qz_stream_t stream);

@@ -20,7 +20,7 @@ QZ_OUT_PACKED_INT32, QZ_OUT_INT8, QZ_OUT_FP8, QZ_OUT_FP4_PACKED, QZ_OUT_FAKEQUAN
 
 QZ_ERR_NULL, QZ_ERR_SHAPE, QZ_ERR_GROUP, QZ_ERR_BLOCK = -1, -2, -3, -4
 QZ_ERR_BITS, QZ_ERR_ASYM_FLOAT, QZ_ERR_FORMAT, QZ_ERR_WORKSPACE, QZ_ERR_ALIGN = -5, -6, -7, -8, -9
-QZ_ERR_UNAVAILABLE, QZ_ERR_CAPACITY = -10, -11
+QZ_ERR_UNAVAILABLE = -10
 
 # every symbol the header declares (tests check the library exports all of them)
 EXPORTS = (
@@ -34,7 +34,7 @@ EXPORTS = (
     "qz_grouped_blocks", "qz_awq_sq_err_partials_count", "qz_awq_sq_err_partials", "qz_awq_sq_err_reduce",
     "qz_awq_sq_err_partials_multi", "qz_awq_stats_layout", "qz_moe_combine",
     "qz_moe_silu_mul", "qz_expert_gemms", "qz_silu_mul", "qz_rmsnorm128",
-    "qz_rotary128", "qz_nvfp4_sync_size", "qz_nvfp4_items_per_slice", "qz_nvfp4_capacity", "qz_quantize_nvfp4",
+    "qz_rotary128", "qz_nvfp4_sync_size", "qz_quantize_nvfp4",
     "qz_quantize_grouped_nvfp4", "qz_expert_gemms_library", "qz_expert_gemms_status",
 )
 
@@ -101,8 +101,6 @@ def load() -> ctypes.CDLL:
         "qz_rmsnorm128": ([P, I64, I64, P, ctypes.c_float, P, P], ctypes.c_int),
         "qz_rotary128": ([P, I64, I64, I64, I64, I64, I64, P, P, I64, I64, P, I64, I64, I64, P], ctypes.c_int),
         "qz_nvfp4_sync_size": ([I64], SZ),
-        "qz_nvfp4_items_per_slice": ([I64, I64], I64),
-        "qz_nvfp4_capacity": ([], I64),
         "qz_quantize_nvfp4": ([P, I64, I64, I64, I64, A, P, P, P, P, SZ, P], ctypes.c_int),
         "qz_quantize_grouped_nvfp4": ([I64, P, I64, I64, A, P, SZ, P], ctypes.c_int),
         "qz_expert_gemms_library": ([ctypes.c_char_p], ctypes.c_int),

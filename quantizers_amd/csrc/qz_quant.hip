@@ -13,8 +13,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdlib>
-#include <mutex>
 
 #include "qz_device.h"
 
@@ -1060,45 +1058,21 @@ __global__ void k_gscale_keys(const uint32_t* tmin, const uint32_t* tmax, int64_
   gs[b] = bfr(bfr(1.0f / am) * 2688.0f);
 }
 
-// --------------------------------------------------------- NVFP4 single-read path
+// ------------------------------------------------------------ NVFP4 fused path (round 4)
 // NVFP4 (TENSOR_GROUP) needs each slice's |w| maximum (its global scale) before any group of
-// that slice can be encoded; the two-pass path above reads every slice twice (a 403 MB fused
-// Qwen3-30B-A3B expert parameter does not fit the 256 MiB MALL, so the second read goes to HBM).
-// k_nv_hold keeps the weight ON CHIP across the per-slice maximum instead: a persistent grid
-// (as many 256-thread workgroups as are resident at once) walks "items" = 64 KiB chunks of the
-// slices, slice-major; workgroup w takes items w, w + G, w + 2G, ...  Per item it loads its
-// 16 units per lane into registers (nt loads, fully coalesced), reduces their |bf16| maximum,
-// publishes it (agent-scope atomic max on the slice's key, then an arrival add on the slice's
-// counter, both executed at the memory side, the second issued after the first returned) and
-// waits until every item of the slice has arrived; then it reads the key, forms the global scale
-// and encodes + stores its held units (process_unit, as the group path).  HBM traffic = one
-// read + one write.
-//
-// Progress: a slice has at most G items, so its items fall in at most two consecutive "rounds"
-// (item / G) and a workgroup waiting in round k only waits for items of rounds k and k + 1;
-// round k + 1's workgroups get there after finishing round k, whose waits never depend on
-// round k + 1 -- with all G workgroups resident nothing can wait forever.
-// Residency is what the occupancy query promises, not a guarantee (another kernel on the
-// device can hold CUs), so every wait is BOUNDED: after spin_ticks of the 100 MHz wall clock
-// the workgroup streams the whole slice itself to get the maximum (slow, still exact) and
-// counts the event in diag[0].  The last item of a slice to leave resets the slice's key and
-// counter, so the sync region is zero after every call (caller contract: zero before the
-// first call).
-#ifndef QZ_NV_PIPE
-#define QZ_NV_PIPE 1  // 1: slices that fit take the pipelined instantiation (A/B knob; 0: the held-only one)
-#endif
-// Two instantiations: PIPE (8 units per lane per item, 32 KiB, the next item's loads in flight
-// while the current one waits: 2 x 32 VGPRs) for slices of up to `capacity` items, and the
-// held-only one (16 units per lane, 64 KiB per item, 64 VGPRs) for slices up to twice that
-// (dense NVFP4 linears such as Qwen3-4B's [9728, 2560] gate / up).
-#ifndef QZ_NV_PIPE_U
-#define QZ_NV_PIPE_U 8  // units per lane per item of the pipelined instantiation (3 buffers)
-#endif
-template <bool PIPE>
-constexpr int nv_units() { return PIPE ? QZ_NV_PIPE_U : 16; }
+// that slice can be encoded.  Two launches, no fills and no separate global-scale launch:
+// k_nv_absmax reduces 32 KiB tiles of every slice into the slice's key (agent-scope atomic max of
+// the |bf16| bits, executed at the memory side), k_nv_encode re-reads each tile, forms the global
+// scale from the key (the launch boundary orders the first launch's atomics before it), encodes
+// and stores codes, e4m3 scales and the global scale; the last tile of a slice to finish resets
+// the slice's key and tile count, so the sync region is zero after every call (caller contract:
+// zero before the first call).  HBM traffic = two reads + one write; a fused Qwen3-30B-A3B expert
+// parameter (403 MB) does not fit the 256 MiB MALL, so no chunking makes the second read cheaper
+// (chunked, register-held and single-launch variants were measured and removed).
 constexpr int NV_BLOCK = 256;
-template <bool PIPE>
-constexpr int64_t nv_chunk() { return (int64_t)NV_BLOCK * nv_units<PIPE>(); }  // units per item
+constexpr int NV_U = 8;                                   // units (8 bf16) per lane per tile
+constexpr int64_t NV_TILE = (int64_t)NV_BLOCK * NV_U;     // 2048 units = 32 KiB of bf16 per workgroup
+constexpr int NV_SYNC_STRIDE = 16;                        // uint32 words per slice: {key, tile count}, one 64-B line
 
 struct NvArgs {
   const uint64_t* tab;  // table mode: DEVICE [4][n_slices] {weight, codes, scales, global scale}; null = batch mode
@@ -1109,177 +1083,101 @@ struct NvArgs {
   float* gs_out;
   int64_t n_slices;
   int64_t units_per_slice;  // rows * cols / 8
-  int64_t items_per_slice;
-  int64_t n_items;
-  uint32_t* sync;  // [n_slices][NV_SYNC_STRIDE]: {key = |bf16| max bits, arrivals + departures, unused...}
-  uint32_t* diag;  // [0]: waits that hit the bound
-  uint64_t spin_ticks;
+  int64_t tiles_per_slice;
+  uint32_t* sync;           // [n_slices][NV_SYNC_STRIDE]
   QP p;
 };
 
-// Sync words are read AT THE MEMORY SIDE, by a compare-exchange that always fails (no sync pair
-// ever holds all ones): a relaxed agent-scope atomic load, or an idempotent RMW (which LLVM turns
-// into one), compiles to a global_load ... sc1 that can be served from this XCD's L2 copy of the
-// line while other XCDs' atomics update it (per-XCD L2s are not coherent).
-// the 8-byte {key, count} pair of a slice, both words in ONE memory-side round trip
-__device__ __forceinline__ uint64_t sync_read2(uint32_t* p) {
-  uint64_t e = ~0ull;
-  __hip_atomic_compare_exchange_strong(reinterpret_cast<uint64_t*>(p), &e, ~0ull - 1, __ATOMIC_RELAXED,
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// A sync word read AT THE MEMORY SIDE, by a compare-exchange that always fails (a key never holds
+// all ones): a relaxed agent-scope atomic load, or an idempotent RMW (which LLVM turns into one),
+// compiles to a global_load ... sc1 that can be served from this XCD's L2 copy of the line while
+// other XCDs' atomics update it (per-XCD L2s are not coherent).
+__device__ __forceinline__ uint32_t sync_read(uint32_t* p) {
+  uint32_t e = 0xffffffffu;
+  __hip_atomic_compare_exchange_strong(p, &e, 0xfffffffeu, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
   return e;
 }
-constexpr int NV_SYNC_STRIDE = 16;  // uint32 words per slice: one 64-B line each
 
 __device__ __forceinline__ uint32_t absmax_bits(const uint4 v) {
   return pk_max_u16(pk_max_u16(v.x & 0x7fff7fffu, v.y & 0x7fff7fffu), pk_max_u16(v.z & 0x7fff7fffu, v.w & 0x7fff7fffu));
 }
 
-#ifndef QZ_NV_PIPE_WAVES
-#define QZ_NV_PIPE_WAVES 3  // minimum waves per SIMD of the pipelined instantiation (VGPR budget)
-#endif
-// held-only: 64 data VGPRs + the encode's; 4 waves per SIMD spills (128-VGPR cap), so 3
-template <bool TAB, bool PIPE>
-__global__ __launch_bounds__(NV_BLOCK, PIPE ? QZ_NV_PIPE_WAVES : 3) void k_nv_hold(NvArgs A) {
-  constexpr int NV_U = nv_units<PIPE>();
-  constexpr int64_t NV_CHUNK = nv_chunk<PIPE>();
-  __shared__ uint32_t red[2][NV_BLOCK / WAVE];  // alternating: arrival k + 2 reuses arrival k's slots
-  __shared__ uint32_t bc[2];
+template <bool TAB>
+__device__ __forceinline__ const uint4* nv_slice(const NvArgs& A, int64_t b) {
+  return TAB ? reinterpret_cast<const uint4*>(A.tab[b]) : reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
+}
+
+// one tile's units, non-temporal (each launch reads a line once); lanes past the slice's end
+// re-read its last unit
+__device__ __forceinline__ void nv_load(uint4 (&v)[NV_U], const uint4* src, int64_t base, int64_t ups, int tid) {
+#pragma unroll
+  for (int u = 0; u < NV_U; ++u) {
+    const int64_t un = min<int64_t>(base + u * NV_BLOCK + tid, ups - 1);
+    v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + un)));
+  }
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(NV_BLOCK) void k_nv_absmax(NvArgs A) {
+  __shared__ uint32_t red[NV_BLOCK / WAVE];
   const int tid = threadIdx.x, lane = tid & (WAVE - 1), wv = tid >> 6;
+  const int64_t b = blockIdx.x / A.tiles_per_slice, base = (blockIdx.x % A.tiles_per_slice) * NV_TILE;
+  uint4 v[NV_U];
+  nv_load(v, nv_slice<TAB>(A, b), base, A.units_per_slice, tid);
+  uint32_t m = 0;
+#pragma unroll
+  for (int u = 0; u < NV_U; ++u) m = pk_max_u16(m, absmax_bits(v[u]));
+  m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
+  if (lane == 0) red[wv] = m;
+  __syncthreads();
+  if (tid == 0)
+    __hip_atomic_fetch_max(A.sync + NV_SYNC_STRIDE * b, max(max(red[0], red[1]), max(red[2], red[3])),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool TAB>
+__global__ __launch_bounds__(NV_BLOCK) void k_nv_encode(NvArgs A) {
+  __shared__ uint32_t keysh;
+  const int tid = threadIdx.x, lane = tid & (WAVE - 1);
+  const int64_t b = blockIdx.x / A.tiles_per_slice, base = (blockIdx.x % A.tiles_per_slice) * NV_TILE;
+  const int64_t ups = A.units_per_slice;
+  uint32_t* sy = A.sync + NV_SYNC_STRIDE * b;
+  uint4 v[NV_U];
+  nv_load(v, nv_slice<TAB>(A, b), base, ups, tid);
+  if (tid == 0) keysh = sync_read(sy);  // final: k_nv_absmax finished before this launch began
+  __syncthreads();
   QP p = A.p;
   p.kind = K_NV;
   p.sym = 1;
-  const int64_t ups = A.units_per_slice, G = gridDim.x, N = A.n_items;
-  const uint32_t n = (uint32_t)A.items_per_slice;
-  auto slice_src = [&](int64_t bb) {
-    return TAB ? reinterpret_cast<const uint4*>(A.tab[bb]) : reinterpret_cast<const uint4*>(A.w + bb * A.ld_batch);
-  };
-  auto load = [&](uint4 (&v)[NV_U], int64_t it) {  // out-of-range lanes re-read the slice's last unit
-    const int64_t bb = it / A.items_per_slice;
-    const int64_t b0 = (it - bb * A.items_per_slice) * NV_CHUNK;
-    const uint4* s0 = slice_src(bb);
-#pragma unroll
-    for (int u = 0; u < NV_U; ++u) {
-      const int64_t un = min<int64_t>(b0 + u * NV_BLOCK + tid, ups - 1);
-      v[u] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s0 + un)));
-    }
-  };
-  int parity = 0;
-  // arrival: the item's |bf16| maximum over the workgroup, then (one lane) an agent-scope max into
-  // the slice's key and an add to its count -- the add depends on the max's RETURNED value (whose
-  // top bit is never set), so the max has been performed at the memory side before it counts
-  auto arrive = [&](const uint4 (&v)[NV_U], int64_t it) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int u = 0; u < NV_U; ++u) m = pk_max_u16(m, absmax_bits(v[u]));
-    m = grp_max_u<WAVE>(max(m & 0xffffu, m >> 16));
-    if (lane == 0) red[parity][wv] = m;
-    __syncthreads();
-    if (tid == 0) {
-      m = max(max(red[parity][0], red[parity][1]), max(red[parity][2], red[parity][3]));
-      uint32_t* sy = A.sync + NV_SYNC_STRIDE * (it / A.items_per_slice);
-      const uint32_t old = __hip_atomic_fetch_max(sy, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(sy + 1, 1u + (old >> 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    parity ^= 1;
-  };
-  // completion: wait until every item of the slice has arrived ({key, count} polled together in
-  // one memory-side CAS: once the count reaches n the key of the same snapshot is final), encode
-  // and store the held units, depart (the slice's last leaver resets its sync words)
-  auto finish = [&](const uint4 (&v)[NV_U], int64_t it) {
-    const int64_t b = it / A.items_per_slice;
-    const int64_t base = (it - b * A.items_per_slice) * NV_CHUNK;
-    uint32_t* sy = A.sync + NV_SYNC_STRIDE * b;
-    if (tid == 0) {
-      uint32_t timed_out = 0;
-      uint64_t kc = sync_read2(sy);
-      if ((uint32_t)(kc >> 32) < n) {
-        const uint64_t t0 = wall_clock64();
-        for (;;) {
-          __builtin_amdgcn_s_sleep(2);
-          kc = sync_read2(sy);
-          if ((uint32_t)(kc >> 32) >= n) break;
-          if (wall_clock64() - t0 > A.spin_ticks) { timed_out = 1; break; }
-        }
-      }
-      bc[0] = timed_out ? 0u : (uint32_t)kc;
-      bc[1] = timed_out;
-    }
-    __syncthreads();
-    uint32_t key = bc[0];
-    const uint4* src = slice_src(b);
-    if (bc[1]) {  // bounded wait expired: the slice's maximum from the slice itself (exact, slow)
-      uint32_t mm = 0;
-      for (int64_t un = tid; un < ups; un += NV_BLOCK) mm = pk_max_u16(mm, absmax_bits(src[un]));
-      mm = grp_max_u<WAVE>(max(mm & 0xffffu, mm >> 16));
-      if (lane == 0) red[parity][wv] = mm;
-      __syncthreads();
-      key = max(max(red[parity][0], red[parity][1]), max(red[parity][2], red[parity][3]));
-      if (tid == 0) __hip_atomic_fetch_add(A.diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-    }
-    FastArgs F;
-    float* gs_out;
-    if constexpr (TAB) {
-      F.q_out = reinterpret_cast<void*>(A.tab[A.n_slices + b]);
-      F.s_out = reinterpret_cast<void*>(A.tab[2 * A.n_slices + b]);
-      gs_out = reinterpret_cast<float*>(A.tab[3 * A.n_slices + b]);
-    } else {
-      F.q_out = reinterpret_cast<uint32_t*>(A.q_out) + b * ups;
-      F.s_out = reinterpret_cast<uint8_t*>(A.s_out) + b * (ups >> 1);
-      gs_out = A.gs_out + b;
-    }
-    F.zp_out = nullptr;
-    F.scale_bytes = 1;
-    F.out_fmt = QZ_OUT_FP4_PACKED;
-    F.col_scales = nullptr;
-    // global scale, k_gscale_keys' arithmetic: bf16(bf16(1 / absmax) * (448 * 6))
-    const float gs = bfr(bfr(1.0f / __uint_as_float(key << 16)) * 2688.0f);
-    if (base == 0 && tid == 0) *gs_out = gs;
-#pragma unroll
-    for (int u = 0; u < NV_U; ++u) {
-      const int64_t local = base + u * NV_BLOCK + tid;
-      process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
-    }
-    if (tid == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == 2u * n - 1u) {
-        __hip_atomic_store(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(sy + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  };
-  int64_t ia = blockIdx.x;
-  if (ia >= N) return;
-  if constexpr (!PIPE) {  // one held item at a time
-    uint4 v[NV_U];
-    for (; ia < N; ia += G) {
-      load(v, ia);
-      arrive(v, ia);
-      finish(v, ia);
-    }
+  // global scale, k_gscale_keys' arithmetic: bf16(bf16(1 / absmax) * (448 * 6))
+  const float gs = bfr(bfr(1.0f / __uint_as_float(keysh << 16)) * 2688.0f);
+  FastArgs F;
+  float* gs_out;
+  if constexpr (TAB) {
+    F.q_out = reinterpret_cast<void*>(A.tab[A.n_slices + b]);
+    F.s_out = reinterpret_cast<void*>(A.tab[2 * A.n_slices + b]);
+    gs_out = reinterpret_cast<float*>(A.tab[3 * A.n_slices + b]);
   } else {
-    // two ARRIVED items held (a: the oldest, b) and one in flight (c): item k + 2 arrives only
-    // after item k is finished, so a slice's wait overlaps the next item's
-    uint4 va[NV_U], vb[NV_U], vc[NV_U];
-    int64_t ib = ia + G, ic = ib + G;
-    load(va, ia);
-    if (ib < N) load(vb, ib);
-    arrive(va, ia);
-    if (ib < N) arrive(vb, ib);
-    if (ic < N) load(vc, ic);
-    for (;;) {
-      finish(va, ia);
-      if (ib >= N) break;
-      ia = ib;
+    F.q_out = reinterpret_cast<uint32_t*>(A.q_out) + b * ups;
+    F.s_out = reinterpret_cast<uint8_t*>(A.s_out) + b * (ups >> 1);
+    gs_out = A.gs_out + b;
+  }
+  F.zp_out = nullptr;
+  F.scale_bytes = 1;
+  F.out_fmt = QZ_OUT_FP4_PACKED;
+  F.col_scales = nullptr;
+  if (base == 0 && tid == 0) *gs_out = gs;
 #pragma unroll
-      for (int u = 0; u < NV_U; ++u) va[u] = vb[u];
-      ib = ic;
-      if (ib >= N) continue;  // one arrived item left
-#pragma unroll
-      for (int u = 0; u < NV_U; ++u) vb[u] = vc[u];
-      ic += G;
-      arrive(vb, ib);
-      if (ic < N) load(vc, ic);
+  for (int u = 0; u < NV_U; ++u) {
+    const int64_t local = base + u * NV_BLOCK + tid;
+    process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
+  }
+  if (tid == 0) {  // the slice's last tile resets its sync words for the next call
+    const uint32_t old = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (uint32_t)A.tiles_per_slice - 1u) {
+      __hip_atomic_store(sy, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sy + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1631,42 +1529,6 @@ WS ws_layout(void* base, int64_t batch, const Plan& pl) {
 }
 size_t ws_size(int64_t batch, const Plan& pl) { return ws_layout(nullptr, batch, pl).bytes; }
 
-// resident 256-thread k_nv_hold workgroups on the current device (occupancy query x CUs, at most
-// 8 per CU: MI355X_MICROARCH.md "Residency"), per instantiation, cached per device
-template <bool TAB, bool PIPE>
-int64_t nv_capacity_of(int dev) {
-  static std::mutex mu;
-  static int64_t cap[64] = {};
-  std::lock_guard<std::mutex> lk(mu);
-  if (cap[dev] == 0) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_nv_hold<TAB, PIPE>, NV_BLOCK, 0) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per_cu <= 0 ||
-        cus <= 0)
-      return 0;
-    cap[dev] = (int64_t)std::min(per_cu, 8) * cus;
-  }
-  return cap[dev];
-}
-int64_t nv_capacity(bool tab, bool pipe) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  if (tab) return pipe ? nv_capacity_of<true, true>(dev) : nv_capacity_of<true, false>(dev);
-  return pipe ? nv_capacity_of<false, true>(dev) : nv_capacity_of<false, false>(dev);
-}
-
-// the bounded wait of k_nv_hold in 100 MHz ticks (default 1 ms); QZ_NV_SPIN_TICKS is a test knob
-// that forces the exact slow path (tests/test_nvfp4_gpu.py)
-uint64_t nv_spin_ticks() {
-  static const uint64_t t = [] {
-    const char* s = getenv("QZ_NV_SPIN_TICKS");
-    return s ? (uint64_t)strtoull(s, nullptr, 10) : (uint64_t)100000;
-  }();
-  return t;
-}
-
-constexpr size_t NV_SYNC_HEAD = 256;  // diag counters, then one 64-B line per slice
-
 int nv_args_ok(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
   if (!a) return QZ_ERR_NULL;
   int rc = make_plan(a, rows, cols, pl);
@@ -1678,29 +1540,17 @@ int nv_args_ok(const qz_args* a, int64_t rows, int64_t cols, Plan* pl) {
 int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st) {
   if (!sync) return QZ_ERR_NULL;
   if (!aligned(sync, 16)) return QZ_ERR_ALIGN;
-  if (sync_bytes < NV_SYNC_HEAD + 4 * NV_SYNC_STRIDE * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
-  // the pipelined instantiation when the slice fits its capacity, else the held-only one
-  bool pipe = QZ_NV_PIPE != 0;
-  int64_t cap = nv_capacity(tab, pipe);
-  if (pipe && cdiv(A.units_per_slice, nv_chunk<true>()) > cap) {
-    pipe = false;
-    cap = nv_capacity(tab, false);
-  }
-  if (cap <= 0) return (int)hipErrorInvalidDevice;
-  A.items_per_slice = cdiv(A.units_per_slice, pipe ? nv_chunk<true>() : nv_chunk<false>());
-  if (A.items_per_slice > cap) return QZ_ERR_CAPACITY;
-  A.n_items = A.n_slices * A.items_per_slice;
-  A.diag = (uint32_t*)sync;
-  A.sync = (uint32_t*)((char*)sync + NV_SYNC_HEAD);
-  A.spin_ticks = nv_spin_ticks();
-  const unsigned grid = (unsigned)std::min<int64_t>(A.n_items, cap);
-  if (tab) {
-    if (pipe) hipLaunchKernelGGL((k_nv_hold<true, true>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
-    else hipLaunchKernelGGL((k_nv_hold<true, false>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
-  } else {
-    if (pipe) hipLaunchKernelGGL((k_nv_hold<false, true>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
-    else hipLaunchKernelGGL((k_nv_hold<false, false>), dim3(grid), dim3(NV_BLOCK), 0, st, A);
-  }
+  if (sync_bytes < 4 * NV_SYNC_STRIDE * (size_t)A.n_slices) return QZ_ERR_WORKSPACE;
+  A.sync = (uint32_t*)sync;
+  A.tiles_per_slice = cdiv(A.units_per_slice, NV_TILE);
+  const int64_t grid = A.n_slices * A.tiles_per_slice;
+  if (grid > 0x7fffffffLL) return QZ_ERR_SHAPE;
+  if (tab) hipLaunchKernelGGL(k_nv_absmax<true>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
+  else hipLaunchKernelGGL(k_nv_absmax<false>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
+  int rc = launch_err();
+  if (rc) return rc;
+  if (tab) hipLaunchKernelGGL(k_nv_encode<true>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
+  else hipLaunchKernelGGL(k_nv_encode<false>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
   return launch_err();
 }
 
@@ -1721,7 +1571,6 @@ const char* qz_strerror(int code) {
     case QZ_ERR_WORKSPACE: return "workspace too small";
     case QZ_ERR_ALIGN: return "alignment requirement violated";
     case QZ_ERR_UNAVAILABLE: return "runtime dependency unavailable (hipBLASLt not loaded or refused the call)";
-    case QZ_ERR_CAPACITY: return "slice larger than the single-read path holds on chip (use qz_quantize)";
   }
   return code > 0 ? hipGetErrorString((hipError_t)code) : "unknown error";
 }
@@ -2050,15 +1899,8 @@ int qz_awq_fake_quant_batched(const void* w, int64_t batch, int64_t rows, int64_
 }
 
 size_t qz_nvfp4_sync_size(int64_t n_slices) {
-  return n_slices < 0 ? 0 : NV_SYNC_HEAD + 4 * NV_SYNC_STRIDE * (size_t)n_slices;
+  return n_slices < 0 ? 0 : 4 * NV_SYNC_STRIDE * (size_t)n_slices;
 }
-
-int64_t qz_nvfp4_items_per_slice(int64_t rows, int64_t cols) {
-  if (rows <= 0 || cols <= 0 || cols % 16) return -1;
-  return cdiv(rows * cols / 8, nv_chunk<true>());
-}
-
-int64_t qz_nvfp4_capacity(void) { return nv_capacity(false, true); }
 
 int qz_quantize_nvfp4(const void* w, int64_t batch, int64_t rows, int64_t cols, int64_t ld_batch, const qz_args* a,
                       void* q_out, void* scale_out, float* gscale_out, void* sync, size_t sync_bytes,

@@ -76,8 +76,8 @@ def stats_workspace(nbytes: int, device) -> torch.Tensor:
 
 
 def sync_workspace(n_slices: int, device, stream=None) -> torch.Tensor:
-    """Per-(device, stream) grow-only sync region of the NVFP4 single-read path
-    (qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4), zeroed when allocated: every call leaves it
+    """Per-(device, stream) grow-only sync region of the NVFP4 path (qz_quantize_nvfp4 /
+    qz_quantize_grouped_nvfp4: each slice's |w| maximum and tile count), zeroed when allocated: every call leaves it
     zero (quantizers_amd.h), and calls on one stream never overlap, so it is shared by them."""
     dev = torch.device(device)
     st = stream if stream is not None else torch.cuda.current_stream(dev)
@@ -91,16 +91,7 @@ def sync_workspace(n_slices: int, device, stream=None) -> torch.Tensor:
     return buf
 
 
-def nvfp4_timeouts(device, stream=None) -> int:
-    """Bounded waits of the NVFP4 single-read kernel that expired on this (device, stream) sync
-    region since it was allocated (diagnostic: 0 when every slice's workgroups were resident)."""
-    dev = torch.device(device)
-    st = stream if stream is not None else torch.cuda.current_stream(dev)
-    buf = _sync_cache.get((dev.index or 0, st.cuda_stream))
-    return 0 if buf is None else int(buf[:4].view(torch.int32).item())
-
-
-def _nvfp4_single_read_ok(a: QuantizationArgs, out_fmt: int, geom, w: torch.Tensor) -> bool:
+def _nvfp4_fused_ok(a: QuantizationArgs, out_fmt: int, geom, w: torch.Tensor) -> bool:
     b, r, c, ld_r, ld_b = geom
     return (a.is_nvfp4 and a.group_size == 16 and out_fmt == _lib.QZ_OUT_FP4_PACKED and ld_r == c
             and (b == 1 or ld_b % 8 == 0) and w.data_ptr() % 16 == 0)
@@ -205,14 +196,13 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
     if a.is_nvfp4 and "global_scale" not in o:
         o["global_scale"] = torch.empty(max(b, 1), dtype=torch.float32, device=dev)
     lib = _lib.load()
-    if _nvfp4_single_read_ok(a, out_fmt, (b, r, c, ld_r, ld_b), w):
+    if _nvfp4_fused_ok(a, out_fmt, (b, r, c, ld_r, ld_b), w):
         sync = sync_workspace(b, dev)
         rc = lib.qz_quantize_nvfp4(_ptr(w), b, r, c, ld_b, ctypes.byref(ca), _ptr(o["codes"]), _ptr(o["scale"]),
                                    _ptr(o["global_scale"]), _ptr(sync), sync.numel(), _stream())
-        if rc != _lib.QZ_ERR_CAPACITY:  # a slice too large to hold on chip: the two-pass path below
-            _lib.check(rc, "qz_quantize_nvfp4")
-            o.pop("workspace", None)
-            return o
+        _lib.check(rc, "qz_quantize_nvfp4")
+        o.pop("workspace", None)
+        return o
     ws_n = lib.qz_quantize_workspace_size(b, r, c, ctypes.byref(ca))
     ws = o.get("workspace")
     if ws is None or ws.numel() < ws_n:
@@ -227,7 +217,7 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
 
 def grouped_ok(a: QuantizationArgs, w: torch.Tensor) -> bool:
     """True when one grouped launch covers this scheme and weight: qz_quantize_grouped (the
-    single-pass group path) or, for NVFP4, qz_quantize_grouped_nvfp4 (the single-read path)."""
+    single-pass group path) or, for NVFP4, qz_quantize_grouped_nvfp4 (two launches per group)."""
     g = a.group_size or 0
     if a.is_nvfp4 and g != 16:
         return False
@@ -334,11 +324,6 @@ class GroupedQuantize:
             sync = sync_workspace(self.n, self.weights[0].device, stream)
             rc = self.lib.qz_quantize_grouped_nvfp4(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
                                                     _ptr(sync), sync.numel(), st)
-            if rc == _lib.QZ_ERR_CAPACITY:  # weights too large to hold on chip: one two-pass launch each
-                with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-                    for w, o in zip(self.weights, self.outs):
-                        quantize_weight(w, self.a, self.out_fmt, out=o)
-                return self.outs
             _lib.check(rc, "qz_quantize_grouped_nvfp4")
             return self.outs
         if self.mixed:

@@ -59,7 +59,7 @@ def main(n=30):
                              ops._ptr(nv_out["global_scale"]), ops._ptr(nv_ws), nv_ws.numel(), ops._stream())
         _lib.check(rc, "qz_quantize")
     kernels += [
-        ("nvfp4_single_read", lambda i: ops.quantize_weight(gus[i % 4][:, :768], nv, out=nv_out), 1),
+        ("nvfp4_fused", lambda i: ops.quantize_weight(gus[i % 4][:, :768], nv, out=nv_out), 1),
         ("nvfp4_two_pass", nv_two_pass, 1),
     ]
     st = torch.cuda.current_stream()

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""NVFP4 single-read (k_nv_hold) vs two-pass (qz_quantize) timing on the reference's NVFP4 shapes:
+"""NVFP4 fused path (qz_quantize_nvfp4: k_nv_absmax + k_nv_encode) vs generic qz_quantize timing on the reference's NVFP4 shapes:
 Qwen3-30B-A3B experts (4 resident layers rotated over 48, as bench.py's MXFP4 leg) and the
 Qwen3-4B dense linears as grouped launches.  HIP events on the launch stream; prints one JSON
 line per case.  Usage: python scripts/nv_probe.py"""
@@ -58,11 +58,11 @@ def main():
                 else:
                     two_pass(w, a)
     npar = 48 * 128 * 3 * 768 * 2048
-    for name, single in (("single_read", True), ("two_pass", False)):
+    for name, single in (("fused", True), ("two_pass", False)):
         t = ev_time(lambda: moe(single))
         gbps = npar * B_PER_PARAM / t / 1e9
         print(json.dumps({"case": f"qwen3_30b_a3b_experts_nvfp4_{name}", "ms": t * 1e3, "params_per_s": npar / t,
-                          "alg_GBps": gbps, "frac": gbps / 8000, "timeouts": ops.nvfp4_timeouts(dev)}), flush=True)
+                          "alg_GBps": gbps, "frac": gbps / 8000}), flush=True)
     # one fused-expert launch alone (the rocprof unit): gate half of layer 0
     w = layers[0][0][:, :768]
     o = outs[(0, 0)]
@@ -82,7 +82,7 @@ def main():
     t = ev_time(lambda: [q.run() for q in gqs])
     gbps = npar * B_PER_PARAM / t / 1e9
     print(json.dumps({"case": "qwen3_4b_dense_nvfp4_grouped", "ms": t * 1e3, "params_per_s": npar / t,
-                      "alg_GBps": gbps, "frac": gbps / 8000, "timeouts": ops.nvfp4_timeouts(dev)}), flush=True)
+                      "alg_GBps": gbps, "frac": gbps / 8000}), flush=True)
     for (r, c), q in zip(by.keys(), gqs):
         tq = ev_time(lambda: q.run())
         nb = q.n * r * c * B_PER_PARAM

@@ -34,8 +34,9 @@ KERNELS = {
     "k_stats_dma<0": ("AWQ absmean [16384, 4096], one launch, LDS-DMA walk (round 4)", T * C * 2),
     "k_stats_dma<1": ("AWQ w_mean [11008, 4096] g128, one launch, LDS-DMA walk (round 4)", P * 2),
     # NVFP4 [128, 768, 2048]: read 2 B + codes 0.5 B + e4m3 scale 1/16 B per param + f32 per slice
-    "k_nv_hold<false>": ("NVFP4 single-read, Qwen3-30B-A3B expert half [128, 768, 2048] (round 4)",
-                         int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
+    "k_nv_encode<false>": ("NVFP4 fused encode launch, Qwen3-30B-A3B expert half [128, 768, 2048] (round 4)",
+                           int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
+    "k_nv_absmax<false>": ("NVFP4 fused |w| max launch [128, 768, 2048] (round 4)", 128 * 768 * 2048 * 2),
     "k_group_fast<1, 3, false, true, true, false>": ("NVFP4 two-pass quantize pass [128, 768, 2048]",
                                                      int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
     "k_absmax_slices": ("NVFP4 two-pass per-slice |w| max pre-pass [128, 768, 2048]", 128 * 768 * 2048 * 2),
