@@ -142,9 +142,9 @@ class CompressionPlan:
     (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
     grouped launch (``ops.GroupedQuantize``: the launch ramp paid once per shape, 5 launches for
     all 252 Qwen3-4B linears; one mixed-shape launch per scheme measured 3 % slower, DESIGN §3);
-    NVFP4 dense units of one shape are one single-read launch (``qz_quantize_grouped_nvfp4``);
-    stacked fused experts, FP8_BLOCK and other schemes are one launch each.  ``run()`` only enqueues the launches (graph/bench
-    friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
+    NVFP4 dense units of one shape are one ``qz_quantize_grouped_nvfp4`` call (two launches);
+    stacked fused experts, FP8_BLOCK and other schemes are one call each.  ``run()`` only enqueues
+    the launches (graph/bench friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
 
     def __init__(self, units: Sequence[CompressUnit], device, stager=None):
         self.device = torch.device(device)

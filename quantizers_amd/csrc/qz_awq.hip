@@ -8,7 +8,6 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 
 #include "qz_device.h"
 
@@ -329,7 +328,7 @@ __device__ __forceinline__ T reduce_rows(T (*red)[WIN], const T* src, int64_t n,
 
 template <int WIN, int SWP, typename T>
 __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int lane, int wv, int64_t C, int64_t nch,
-                                             int64_t cpg, T* part, T* gpart, unsigned* cnt, T* sum) {
+                                             int64_t cpg, T* part, T* gpart, unsigned* cnt, T* sum, T pre) {
   constexpr int LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, NT = SWP * 64, TF = NT / WIN;
   static_assert(TF >= 1 && NT % WIN == 0 && S >= TF, "stats window");
   const int q = lane / LPR, c8 = lane % LPR;
@@ -354,13 +353,22 @@ __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int la
   const T vg = reduce_rows<WIN, NT>(red, part + g0 * C, n_g, C, cb);  // this group's chunks
   const bool out_thread = threadIdx.x < WIN && cb + threadIdx.x < C;
   if (ng == 1) {
-    if (out_thread) sum[cb + threadIdx.x] += vg;
+    if (out_thread) sum[cb + threadIdx.x] = pre + vg;
     return;
   }
   if (out_thread) st_coherent(gpart + g * C + cb + threadIdx.x, vg);
   if (!arrive_last(wc + ng, (unsigned)ng)) return;
   const T v = reduce_rows<WIN, NT>(red, gpart, ng, C, cb);  // the groups, in order
-  if (out_thread) sum[cb + threadIdx.x] += v;
+  if (out_thread) sum[cb + threadIdx.x] = pre + v;
+}
+
+// the window's running sums, read when the workgroup starts: the last arriver's final add then
+// waits for no load (only that workgroup writes them, after every workgroup of the window has
+// started, so every copy is the value before this launch)
+template <int WIN, typename T>
+__device__ __forceinline__ T stats_pre(const T* sum, int64_t C) {
+  const int64_t c = (int64_t)blockIdx.x * WIN + threadIdx.x;
+  return (threadIdx.x < WIN && c < C) ? sum[c] : T(0);
 }
 
 template <int WIN>
@@ -373,6 +381,7 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
   const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
+  const float pre = stats_pre<WIN>(sum, C);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   auto row = [&](const uint4 v, bool ok) {
     const uint32_t w[4] = {ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u};
@@ -383,7 +392,7 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
     }
   };
   stats_walk<S, QZ_ABS1_NB, QZ_ABS1_PP>(x + c0, ld, t0 + wv * RPW, q, t1, row);
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum, pre);
 }
 
 typedef float qz_f32x2 __attribute__((ext_vector_type(2)));
@@ -405,6 +414,7 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
   const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
+  const double pre = stats_pre<WIN>(wsum, C);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto row = [&](const uint4 v, bool ok) {
     const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
@@ -420,119 +430,7 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
     }
   };
   stats_walk<S, QZ_WM1_NB, QZ_WM1_PP>(w + c0, ld, r0 + wv * RPW, q, r1, row);
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum);
-}
-
-// ------------------------------------- a3 / a4, one launch, LDS-DMA walk (round 4)
-// The one-launch kernels above keep their loads in VGPRs, which caps the bytes in flight (w_mean:
-// 2 waves per SIMD x 8 loads of 16 B) and forces 128-column windows (256-B row segments) to get
-// enough workgroups.  Here each wave streams its rows with global_load_lds_dwordx4 into a private
-// LDS ring of DMA_D slots (1 KiB = one 512-column row segment per slot), so a wave keeps DMA_D KiB
-// in flight at no VGPR cost and every wave-load is one contiguous 1 KiB; the ring is read back
-// with ds_read_b128 (inline asm: the compiler's own wait before an LDS read that may alias a DMA
-// is a full vmcnt(0), which would drain the ring every row), a slot refilled as soon as it has
-// been read.  Window = 512 columns, slot = wave (S = DMA_NW rows in flight per workgroup-step,
-// row r0 + w, r0 + w + S, ... for wave w), the ring memory reused for stats_finish's reduction:
-// the same fixed-order tree as the kernels above with WIN = 512, RPW = 1, TF = 1.
-#ifndef QZ_STATS_DMA
-#define QZ_STATS_DMA 0  // 1: the LDS-DMA walk for aligned absmean / w_mean; 0: k_absmean_1l / k_wmean_1l (A/B)
-#endif
-#ifndef QZ_DMA_D
-#define QZ_DMA_D 8  // ring slots (KiB in flight) per wave
-#endif
-#ifndef QZ_DMA_BLOCKS
-#define QZ_DMA_BLOCKS 256  // target workgroups (8 waves, 64 KiB of LDS each)
-#endif
-#ifndef QZ_DMA_AUX
-#define QZ_DMA_AUX 0  // cache policy of the DMA loads (2 = nt)
-#endif
-constexpr int DMA_NW = 8, DMA_D = QZ_DMA_D, DMA_WIN = 512;
-
-__device__ __forceinline__ uint4 lds_read16(const void* p) {
-  const uint32_t a = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-  qz_u32x4 t;
-  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(t) : "v"(a) : "memory");
-  return make_uint4(t.x, t.y, t.z, t.w);
-}
-
-// rows first, first + NW, ... < r1 of this lane's 8 columns (col = column pointer) through the
-// wave's ring (D slots of 64 x 16 B); f(v) per row, in row order
-template <int NW, int D, typename F>
-__device__ __forceinline__ void stats_walk_dma(const uint16_t* col, int64_t ld, int64_t first, int64_t r1, int lane,
-                                               uint4 (*ring)[64], F&& f) {
-  if (first >= r1) return;
-  const int64_t n = (r1 - first + NW - 1) / NW;  // rows of this wave (wave-uniform)
-  auto issue = [&](int64_t i, int slot) {
-    __builtin_amdgcn_global_load_lds((const void*)(col + (first + i * NW) * ld),
-                                     (__attribute__((address_space(3))) void*)&ring[slot][0], 16, 0, QZ_DMA_AUX);
-  };
-#pragma unroll
-  for (int j = 0; j < D; ++j)
-    if (j < n) issue(j, j);
-  int64_t i = 0;
-  for (; i + 2 * D <= n; i += D) {  // steady state: every refill is a row of this wave
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D - 1) : "memory");  // row i + j has landed
-      const uint4 v = lds_read16(&ring[j][lane]);
-      issue(i + D + j, j);
-      f(v);
-    }
-  }
-  // tail: at most D rows in flight, fewer than D more to load
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int j = 0; j < D; ++j)
-    if (i + j < n) f(lds_read16(&ring[j][lane]));
-  i += D;
-  if (i < n) {
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-      if (i + j < n) issue(i + j, j);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < D; ++j)
-      if (i + j < n) f(lds_read16(&ring[j][lane]));
-  }
-}
-
-// KIND 0: absmean (f32 sums of |x|); 1: w_mean (f64 sums of bf16(|w| / bf16(group absmax + 1e-6)))
-template <int KIND, int LOGL>
-__global__ __launch_bounds__(DMA_NW * 64) void k_stats_dma(const uint16_t* x, int64_t R, int64_t C, int64_t ld,
-                                                           int64_t rc, int64_t nch, int64_t cpg, void* part_,
-                                                           void* gpart_, unsigned* cnt, void* sum_) {
-  using T = typename std::conditional<KIND == 0, float, double>::type;
-  constexpr int L = 1 << LOGL;
-  static_assert(L <= 64, "a group inside one 512-column row segment");
-  static_assert(sizeof(T) * DMA_NW * DMA_WIN <= sizeof(uint4) * DMA_NW * DMA_D * 64, "reduction fits the ring");
-  __shared__ uint4 ring[DMA_NW][DMA_D][64];
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * DMA_WIN + lane * 8, C - 8);
-  const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
-  T acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  stats_walk_dma<DMA_NW, DMA_D>(x + c0, ld, r0 + wv, r1, lane, ring[wv], [&](const uint4 v) {
-    if constexpr (KIND == 0) {
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += fabsf(__uint_as_float(w[k] << 16));
-        acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
-      }
-    } else {
-      const uint32_t u[4] = {v.x & 0x7fff7fffu, v.y & 0x7fff7fffu, v.z & 0x7fff7fffu, v.w & 0x7fff7fffu};
-      const uint32_t pm = pk_max_u16(pk_max_u16(u[0], u[1]), pk_max_u16(u[2], u[3]));
-      const float m = __uint_as_float(grp_max_u<L>(max(pm & 0xffffu, pm >> 16)) << 16);
-      const float rd = __builtin_amdgcn_rcpf(bfr(m + 1e-6f));  // rcp lemma: bf16(|w| * rd) == bf16(|w| / d)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += (double)bfr(__uint_as_float(u[k] << 16) * rd);
-        acc[2 * k + 1] += (double)bfr(__uint_as_float(u[k] & 0xffff0000u) * rd);
-      }
-    }
-  });
-  __syncthreads();  // every wave is done with its ring: the memory becomes the reduction buffer
-  stats_finish<DMA_WIN, DMA_NW>(reinterpret_cast<T(*)[DMA_WIN]>(&ring[0][0][0]), acc, lane, wv, C, nch, cpg, (T*)part_,
-                                (T*)gpart_, cnt, (T*)sum_);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum, pre);
 }
 
 // chunking of the one-launch kernels: >= min_rc rows per chunk, about `blocks` workgroups
@@ -542,13 +440,10 @@ int64_t stats1_chunks(int64_t R, int64_t C, int win, int64_t blocks, int64_t min
   *rc = cdiv(R, n);
   return cdiv(R, *rc);
 }
-int wmean_win(int64_t g) {
-  return QZ_STATS_DMA ? DMA_WIN : (int)std::min<int64_t>(512, std::max<int64_t>(QZ_WM1_WIN, g));
-}
-constexpr int ABS1_WIN = QZ_STATS_DMA ? DMA_WIN : QZ_ABS1_WIN;
-constexpr int ABS1_SWP = QZ_STATS_DMA ? DMA_NW : QZ_ABS1_WPB;
-constexpr int WM1_SWP = QZ_STATS_DMA ? DMA_NW : QZ_WM1_WPB;
-constexpr int64_t DMA_MIN_RC = 4 * DMA_NW;  // rows per chunk at least: 4 per wave
+int wmean_win(int64_t g) { return (int)std::min<int64_t>(512, std::max<int64_t>(QZ_WM1_WIN, g)); }
+constexpr int ABS1_WIN = QZ_ABS1_WIN;
+constexpr int ABS1_SWP = QZ_ABS1_WPB;
+constexpr int WM1_SWP = QZ_WM1_WPB;
 // workspace bytes of a one-launch statistics call: counters | chunk partials | group partials
 int64_t stats1_bytes(int64_t nch, int64_t C, int64_t elem) {
   return STATS_HEAD + elem * (nch + cdiv(nch, QZ_STATS_CPG)) * C;
@@ -835,8 +730,7 @@ extern "C" {
 // one-launch plan of an absmean call (chunks), or -1 when the counters do not fit (two-launch path)
 static int64_t absmean_1l(int64_t tokens, int64_t channels, int64_t* tc) {
   if (!QZ_STATS_1L) return -1;
-  const int64_t n1 = QZ_STATS_DMA ? stats1_chunks(tokens, channels, ABS1_WIN, QZ_DMA_BLOCKS, DMA_MIN_RC, tc)
-                                  : stats1_chunks(tokens, channels, ABS1_WIN, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, tc);
+  const int64_t n1 = stats1_chunks(tokens, channels, ABS1_WIN, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, tc);
   return stats1_counters_fit(channels, ABS1_WIN, n1) ? n1 : -1;
 }
 
@@ -863,16 +757,9 @@ int qz_awq_absmean_accum(const void* x, int64_t tokens, int64_t channels, int64_
   float* part = (float*)workspace;
   const bool v8 = channels % 8 == 0 && ld % 8 == 0 && aligned(x, 16) && aligned(workspace, 16) &&
                   tokens < INT32_MAX && ld < INT32_MAX;
-  if (v8 && n1 > 0 && QZ_STATS_DMA) {
-    float* p1 = (float*)((char*)workspace + STATS_HEAD);
-    hipLaunchKernelGGL((k_stats_dma<0, 0>), dim3((unsigned)cdiv(channels, DMA_WIN), (unsigned)n1), dim3(DMA_NW * 64), 0,
-                       st, (const uint16_t*)x, tokens, channels, ld, tc1, n1, (int64_t)QZ_STATS_CPG, (void*)p1,
-                       (void*)(p1 + n1 * channels), (unsigned*)workspace, (void*)sum);
-    return launch_err();
-  }
   if (v8 && n1 > 0) {
     float* p1 = (float*)((char*)workspace + STATS_HEAD);
-    hipLaunchKernelGGL(k_absmean_1l<(QZ_STATS_DMA ? QZ_ABS1_WIN : ABS1_WIN)>, dim3((unsigned)cdiv(channels, ABS1_WIN), (unsigned)n1),
+    hipLaunchKernelGGL(k_absmean_1l<ABS1_WIN>, dim3((unsigned)cdiv(channels, ABS1_WIN), (unsigned)n1),
                        dim3(QZ_ABS1_WPB * 64), 0, st, (const uint16_t*)x, tokens, channels, ld, tc1, n1,
                        (int64_t)QZ_STATS_CPG, p1, p1 + n1 * channels, (unsigned*)workspace, sum);
     return launch_err();
@@ -973,8 +860,7 @@ int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part
 static int64_t wmean_1l(int64_t rows, int64_t cols, int64_t g, int64_t* rc) {
   if (!QZ_STATS_1L || g < 8 || g > 512 || (g & (g - 1))) return -1;
   const int win = wmean_win(g);
-  const int64_t n1 = QZ_STATS_DMA ? stats1_chunks(rows, cols, win, QZ_DMA_BLOCKS, DMA_MIN_RC, rc)
-                                  : stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, rc);
+  const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, rc);
   return stats1_counters_fit(cols, win, n1) ? n1 : -1;
 }
 
@@ -1027,26 +913,6 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
     const uint16_t* wp = (const uint16_t*)w;
     int64_t rc1;
     const int64_t n1 = wmean_1l(rows, cols, g, &rc1);
-    if (n1 > 0 && QZ_STATS_DMA) {
-      dim3 grid1((unsigned)cdiv(cols, DMA_WIN), (unsigned)n1), blk1(DMA_NW * 64);
-      double* p1 = (double*)((char*)workspace + STATS_HEAD);
-      void* gp = p1 + n1 * cols;
-      const int64_t cpg = QZ_STATS_CPG;
-      unsigned* cnt = (unsigned*)workspace;
-      switch (logl) {
-#define QZ_DMA_WM(LG) hipLaunchKernelGGL((k_stats_dma<1, LG>), grid1, blk1, 0, st, wp, rows, cols, ld, rc1, n1, cpg, \
-                                         (void*)p1, gp, cnt, (void*)wsum)
-        case 0: QZ_DMA_WM(0); break;
-        case 1: QZ_DMA_WM(1); break;
-        case 2: QZ_DMA_WM(2); break;
-        case 3: QZ_DMA_WM(3); break;
-        case 4: QZ_DMA_WM(4); break;
-        case 5: QZ_DMA_WM(5); break;
-        default: QZ_DMA_WM(6); break;
-#undef QZ_DMA_WM
-      }
-      return launch_err();
-    }
     if (n1 > 0) {
       const int win = wmean_win(g);
       dim3 grid1((unsigned)cdiv(cols, win), (unsigned)n1), blk1(QZ_WM1_WPB * 64);

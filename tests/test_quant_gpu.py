@@ -697,8 +697,9 @@ def test_quantize_grouped_rejects(cuda):
     import ctypes
     nv = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16)
     w = _edge_weight(32, 256, 16, seed=1).to(cuda)
-    with pytest.raises(ValueError):
-        ops.GroupedQuantize([w], nv)
+    w2 = _edge_weight(64, 256, 16, seed=2).to(cuda)
+    with pytest.raises(ValueError):  # NVFP4 groups one shape per call (qz_quantize_grouped_nvfp4)
+        ops.GroupedQuantize([w, w2], nv)
     a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
     lib = _lib.load()
     tab = torch.zeros(4, dtype=torch.int64, device=cuda)
