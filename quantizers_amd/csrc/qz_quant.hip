@@ -1136,6 +1136,41 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_absmax(NvArgs A) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One unit (8 bf16; a group of 16 = two lanes) of a slice with a finite global scale: the
+// arithmetic of group_params(K_NV) + encode_store, with (a) the e4m3 scale code from
+// v_cvt_pk_fp8_f32 (RNE; the FP8 path's conversion, exhaustively checked on bf16 inputs: s32 =
+// gs * s is an exact product of two bf16 in [0, 448]) and (b) the code's dense scale sf / gs and
+// its reciprocal from the workgroup's 128-entry tables (ts, trs: the same IEEE division and rcp,
+// done once per code instead of once per group; trs = 0 where the rcp is not accurate, which sends
+// every element of the group to the IEEE division, as g.fast == false does).  A per-unit instead of
+// per-pair boundary branch in encode_store measured slower (158 vs 150 us per [128, 768, 2048],
+// profiles/r04n_nvprobe_*.log).
+__device__ __forceinline__ void nv_unit(const FastArgs& F, const QP& p, const uint4 v, int64_t unit, bool valid,
+                                        float gs, int lane, const float* ts, const float* trs) {
+  const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
+  f32x2 x[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    x[k].x = __uint_as_float(wd[k] << 16);
+    x[k].y = __uint_as_float(wd[k] & 0xffff0000u);
+  }
+  const uint32_t m = pk_max_u16(pk_max_u16(wd[0] & 0x7fff7fffu, wd[1] & 0x7fff7fffu),
+                                pk_max_u16(wd[2] & 0x7fff7fffu, wd[3] & 0x7fff7fffu));
+  const float am = __uint_as_float(grp_max_u<2>(max(m & 0xffffu, m >> 16) << 16));
+  const float s = (am == 0.f) ? 0.f : bf16_quot(am, p.half_range, p.inv_half);
+  uint32_t s8 = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(fminf(gs * s, 448.f), 0.f, 0, false) & 0xffu;
+  if (s8 == 0) s8 = 0x20u;  // eps of float8_e4m3fn (D1)
+  GP g;
+  g.sbits = s8;
+  g.s = ts[s8];
+  g.rs = trs[s8];
+  g.zp = 0.f;
+  g.fast = true;
+  if (!valid) return;
+  encode_store<K_NV, false, true, true>(F, p, g, x, nullptr, unit);
+  if ((lane & 1) == 0) reinterpret_cast<uint8_t*>(F.s_out)[unit >> 1] = (uint8_t)s8;
+}
+
 template <bool TAB>
 __global__ __launch_bounds__(NV_BLOCK) void k_nv_encode(NvArgs A) {
   __shared__ uint32_t keysh;
@@ -1168,10 +1203,25 @@ __global__ __launch_bounds__(NV_BLOCK) void k_nv_encode(NvArgs A) {
   F.out_fmt = QZ_OUT_FP4_PACKED;
   F.col_scales = nullptr;
   if (base == 0 && tid == 0) *gs_out = gs;
+  if (__builtin_isfinite(gs)) {  // workgroup-uniform
+    __shared__ float ts[128], trs[128];
+    if (tid < 128) {
+      const float sc = e4m3_to_f32((uint32_t)tid) / gs;  // _quantize: scale / global_scale (f32)
+      ts[tid] = sc;
+      trs[tid] = (sc >= 0x1.0p-100f && sc <= 0x1.0p+100f) ? __builtin_amdgcn_rcpf(sc) : 0.f;
+    }
+    __syncthreads();
 #pragma unroll
-  for (int u = 0; u < NV_U; ++u) {
-    const int64_t local = base + u * NV_BLOCK + tid;
-    process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
+    for (int u = 0; u < NV_U; ++u) {
+      const int64_t local = base + u * NV_BLOCK + tid;
+      nv_unit(F, p, v[u], local, local < ups, gs, lane, ts, trs);
+    }
+  } else {  // an all-zero (or non-finite) slice: the general arithmetic
+#pragma unroll
+    for (int u = 0; u < NV_U; ++u) {
+      const int64_t local = base + u * NV_BLOCK + tid;
+      process_unit<1, K_NV, false, true, true>(F, p, v[u], local, local < ups, gs, lane, 0, nullptr);
+    }
   }
   if (tid == 0) {  // the slice's last tile resets its sync words for the next call
     const uint32_t old = __hip_atomic_fetch_add(sy + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1,0 +1,7 @@
+export TMPDIR=/tmp
+T=quantizers_amd/csrc/build/tune
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_nvfp4_gpu.py tests/test_quant_gpu.py -k "nvfp4 or tensor_group or stats or absmean or wmean or weight_mean or fused_experts or small_slices or grouped_dense or larger_than or two_streams" > gpurun_out/r04m_tests.log 2>&1 || { tail -30 gpurun_out/r04m_tests.log; exit 1; }
+tail -2 gpurun_out/r04m_tests.log
+timeout -k 10 300 python -u scripts/tune_stats.py $T/libqz_base.so $T/libqz_pre.so > gpurun_out/r04m_tune_stats.log 2>&1 || exit 1
+tail -2 gpurun_out/r04m_tune_stats.log
+for v in pre nvtab pre nvtab; do QUANTIZERS_AMD_LIB=$T/libqz_$v.so timeout -k 10 300 python -u scripts/nv_probe.py > gpurun_out/r04m_nvprobe_$v.log 2>&1 || exit 1; grep -E "one_launch|experts_nvfp4_fused|dense" gpurun_out/r04m_nvprobe_$v.log | sed "s/^/$v /"; done
