@@ -163,9 +163,6 @@ __global__ __launch_bounds__(FW * 64) void k_colsum_final(const T* part, int64_t
 constexpr int STATS_CNT = 8192;  // arrival counters (uint32) at the head of a statistics workspace
 constexpr int64_t STATS_HEAD = (int64_t)STATS_CNT * 4;
 static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics workspace (quantizers_amd.h)");
-#ifndef QZ_STATS_1L
-#define QZ_STATS_1L 1  // 1: one-launch statistics; 0: the two-launch kernels above (A/B knob)
-#endif
 #ifndef QZ_STATS_CPG
 #define QZ_STATS_CPG 32  // tuning knob: chunks per first-level reduction group
 #endif
@@ -190,12 +187,6 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #ifndef QZ_WM1_WPB
 #define QZ_WM1_WPB 8
 #endif
-#ifndef QZ_WM1_PP
-#define QZ_WM1_PP 0  // tuning knob: w_mean walk with two register sets in turn (same time, more VGPRs)
-#endif
-#ifndef QZ_ABS1_PP
-#define QZ_ABS1_PP 0  // tuning knob: absmean walk with two register sets in turn
-#endif
 #ifndef QZ_WM1_NB
 #define QZ_WM1_NB 4
 #endif
@@ -208,15 +199,13 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 
 // rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per
 // batch, the next batch loaded before the current one is used; f(v, valid) per row in order.  rb
-// is wave-uniform; every row of a batch that is followed by another batch is valid.  PP: two
-// register sets used in turn (no copies between them, but the loop body twice: more VGPRs --
-// taken by w_mean, whose grid is 2 waves per SIMD anyway); otherwise the next batch is copied
-// into the current one (absmean: 8 waves per SIMD need the VGPRs).
+// is wave-uniform; every row of a batch that is followed by another batch is valid.  (Two
+// register sets used in turn instead of the copy measured the same time with more VGPRs.)
 #ifndef QZ_STATS_NT
 #define QZ_STATS_NT 1  // non-temporal 16-B loads in the one-launch statistics walk: absmean 26.2 -> 25.0 us,
                         // w_mean 19.4 -> 18.1 us back to back, same bits (profiles/r04d_tune_stats.log)
 #endif
-template <int S, int SNB, bool PP, typename F>
+template <int S, int SNB, typename F>
 __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int64_t rb, int q, int64_t r1, F&& f) {
   if (rb >= r1) return;
   const uint32_t rlast = (uint32_t)(r1 - 1), uld = (uint32_t)ld;
@@ -232,42 +221,16 @@ __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int
   uint4 a[SNB], b[SNB];
 #pragma unroll
   for (int j = 0; j < SNB; ++j) a[j] = ld16(rb + q + (int64_t)j * S);
-  if constexpr (!PP) {
-    for (; rb + STEP < r1; rb += STEP) {
+  for (; rb + STEP < r1; rb += STEP) {
 #pragma unroll
-      for (int j = 0; j < SNB; ++j) b[j] = ld16(rb + STEP + q + (int64_t)j * S);
+    for (int j = 0; j < SNB; ++j) b[j] = ld16(rb + STEP + q + (int64_t)j * S);
 #pragma unroll
-      for (int j = 0; j < SNB; ++j) f(a[j], true);
+    for (int j = 0; j < SNB; ++j) f(a[j], true);
 #pragma unroll
-      for (int j = 0; j < SNB; ++j) a[j] = b[j];
-    }
-#pragma unroll
-    for (int j = 0; j < SNB; ++j) f(a[j], rb + q + (int64_t)j * S < r1);
-    return;
-  } else {
-    while (true) {
-      if (rb + STEP >= r1) {
-#pragma unroll
-        for (int j = 0; j < SNB; ++j) f(a[j], rb + q + (int64_t)j * S < r1);
-        return;
-      }
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) b[j] = ld16(rb + STEP + q + (int64_t)j * S);
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) f(a[j], true);
-      rb += STEP;
-      if (rb + STEP >= r1) {
-#pragma unroll
-        for (int j = 0; j < SNB; ++j) f(b[j], rb + q + (int64_t)j * S < r1);
-        return;
-      }
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) a[j] = ld16(rb + STEP + q + (int64_t)j * S);
-#pragma unroll
-      for (int j = 0; j < SNB; ++j) f(b[j], true);
-      rb += STEP;
-    }
+    for (int j = 0; j < SNB; ++j) a[j] = b[j];
   }
+#pragma unroll
+  for (int j = 0; j < SNB; ++j) f(a[j], rb + q + (int64_t)j * S < r1);
 }
 
 // Memory ordering without a device-scope fence (an agent-scope release writes the whole L2 back
@@ -391,7 +354,7 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
       acc[2 * k + 1] += fabsf(__uint_as_float(w[k] & 0xffff0000u));
     }
   };
-  stats_walk<S, QZ_ABS1_NB, QZ_ABS1_PP>(x + c0, ld, t0 + wv * RPW, q, t1, row);
+  stats_walk<S, QZ_ABS1_NB>(x + c0, ld, t0 + wv * RPW, q, t1, row);
   stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum, pre);
 }
 
@@ -429,7 +392,7 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
       acc[2 * k + 1] += (double)bfr1(__uint_as_float(u[k] & 0xffff0000u) * rd);
     }
   };
-  stats_walk<S, QZ_WM1_NB, QZ_WM1_PP>(w + c0, ld, r0 + wv * RPW, q, r1, row);
+  stats_walk<S, QZ_WM1_NB>(w + c0, ld, r0 + wv * RPW, q, r1, row);
   stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum, pre);
 }
 
@@ -729,7 +692,6 @@ extern "C" {
 
 // one-launch plan of an absmean call (chunks), or -1 when the counters do not fit (two-launch path)
 static int64_t absmean_1l(int64_t tokens, int64_t channels, int64_t* tc) {
-  if (!QZ_STATS_1L) return -1;
   const int64_t n1 = stats1_chunks(tokens, channels, ABS1_WIN, QZ_ABS1_BLOCKS, QZ_ABS1_MIN_RC, tc);
   return stats1_counters_fit(channels, ABS1_WIN, n1) ? n1 : -1;
 }
@@ -858,7 +820,7 @@ int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part
 
 // one-launch plan of a w_mean call (chunks), or -1 (two-launch / generic paths)
 static int64_t wmean_1l(int64_t rows, int64_t cols, int64_t g, int64_t* rc) {
-  if (!QZ_STATS_1L || g < 8 || g > 512 || (g & (g - 1))) return -1;
+  if (g < 8 || g > 512 || (g & (g - 1))) return -1;
   const int win = wmean_win(g);
   const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, rc);
   return stats1_counters_fit(cols, win, n1) ? n1 : -1;

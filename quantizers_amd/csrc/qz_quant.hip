@@ -172,9 +172,6 @@ __device__ __forceinline__ float bf16_div(float d, float c) {
 #ifndef QZ_SC1
 #define QZ_SC1 2  // 0 = plain stores, 1 = sc1 code + scale stores, 2 = sc1 code stores
 #endif
-#ifndef QZ_SC1_NT
-#define QZ_SC1_NT 0  // sc1 instead of nt code stores in the nt path (tuning knob)
-#endif
 // sc1 store (relaxed agent-scope atomic store = global_store_* sc1)
 template <typename T>
 __device__ __forceinline__ void st_sc1(T* p, const T v) {
@@ -195,9 +192,9 @@ __device__ __forceinline__ void st_sc1(T* p, const T v) {
 // output stores; NTS = non-temporal (streaming outputs of launches far larger than the MALL)
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_out(T* p, const T v) {
-  if constexpr (((QZ_SC1 != 0 && !NTS) || (QZ_SC1_NT && NTS)) && sizeof(T) <= 8) {
+  if constexpr (QZ_SC1 != 0 && !NTS && sizeof(T) <= 8) {
     st_sc1(p, v);
-  } else if constexpr (((QZ_SC1 != 0 && !NTS) || (QZ_SC1_NT && NTS)) && sizeof(T) == 16) {
+  } else if constexpr (QZ_SC1 != 0 && !NTS && sizeof(T) == 16) {
     st16_wt(p, __builtin_bit_cast(uint4, v));
   } else if constexpr (NTS) {
     if constexpr (sizeof(T) == 4) {
@@ -242,21 +239,26 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
   // 21 mantissa bits are within 4 of zero (mod 2^21); such pairs (and +-0, which needs the
   // signed-zero rule) take the IEEE division.  Exact grid values may be flagged too (harmless).
   if (KIND == K_NV && !FQ && QZ_HW_FP4) {
-    uint32_t word = 0;
+    // near: the low 21 bits of (bits + 4) below 8, i.e. ((bits << 11) + (4 << 11)) < (8 << 11)
+    // (one v_lshl_add_u32 each), either element of the pair (v_min_u32); each pair's two codes
+    // go straight into byte k of the word (the conversion's destination-byte select)
+    float ca[4], cb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float qa = x[k].x * g.rs, qb = x[k].y * g.rs;
-      const bool near = (((__float_as_uint(qa) + 4u) & 0x1fffffu) < 8u) | (((__float_as_uint(qb) + 4u) & 0x1fffffu) < 8u);
-      uint32_t pk;
+      const bool near = min((__float_as_uint(qa) << 11) + 0x2000u, (__float_as_uint(qb) << 11) + 0x2000u) < 0x4000u;
       if (__builtin_expect(near || !g.fast, 0)) {
-        pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, __builtin_amdgcn_fmed3f(x[k].x / g.s, -6.f, 6.f) + 0.0f,
-                                                      __builtin_amdgcn_fmed3f(x[k].y / g.s, -6.f, 6.f) + 0.0f, 1.0f, 0);
+        ca[k] = __builtin_amdgcn_fmed3f(x[k].x / g.s, -6.f, 6.f) + 0.0f;
+        cb[k] = __builtin_amdgcn_fmed3f(x[k].y / g.s, -6.f, 6.f) + 0.0f;
       } else {
-        pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, __builtin_amdgcn_fmed3f(qa, -6.f, 6.f),
-                                                      __builtin_amdgcn_fmed3f(qb, -6.f, 6.f), 1.0f, 0);
+        ca[k] = __builtin_amdgcn_fmed3f(qa, -6.f, 6.f);
+        cb[k] = __builtin_amdgcn_fmed3f(qb, -6.f, 6.f);
       }
-      word |= (pk & 0xffu) << (8 * k);
     }
+    uint32_t word = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, ca[0], cb[0], 1.0f, 0);
+    word = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(word, ca[1], cb[1], 1.0f, 1);
+    word = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(word, ca[2], cb[2], 1.0f, 2);
+    word = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(word, ca[3], cb[3], 1.0f, 3);
     st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, word);
     return;
   }
@@ -307,24 +309,11 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
     } else if (A.out_fmt == QZ_OUT_PACKED_INT32 && p.bits == 4) {
       // the low byte of each float 0x4B0000uu is its code u (< 16): gather the even elements'
       // bytes into E and the odd ones' into O (v_perm_b32), word = E | O << 4 (7 VALU for 8 codes)
-#ifndef QZ_PERM_PACK
-#define QZ_PERM_PACK 1
-#endif
-#if !QZ_PERM_PACK
-      uint32_t acc = 0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc += __float_as_uint(q[k].x) << (8 * k);
-        acc += __float_as_uint(q[k].y) << (8 * k + 4);
-      }
-      st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, acc - 0xFB000000u);
-#else
       const uint32_t e_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].x), __float_as_uint(q[0].x), 0x0c0c0400u);
       const uint32_t e_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].x), __float_as_uint(q[2].x), 0x04000c0cu);
       const uint32_t o_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].y), __float_as_uint(q[0].y), 0x0c0c0400u);
       const uint32_t o_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].y), __float_as_uint(q[2].y), 0x04000c0cu);
       st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, ((o_lo | o_hi) << 4) | (e_lo | e_hi));
-#endif
     } else {
       uint32_t c[8];
 #pragma unroll
@@ -514,20 +503,10 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
     // table entries are global-memory pointers; casting through address space 1 makes the
     // compiler emit global_* instead of flat_* loads and stores, which measured SLOWER here
     // (grouped int4 g128, 100 weights: 17.09 -> 18.16 us/weight, r02g A/B), so flat it stays
-#ifndef QZ_TAB_GLOBAL
-#define QZ_TAB_GLOBAL 0
-#endif
-#if QZ_TAB_GLOBAL
-    A.w = (const uint16_t*)(const __attribute__((address_space(1))) uint16_t*)A0.tab[b];
-    A.q_out = (void*)(__attribute__((address_space(1))) char*)A0.tab[A0.n_tab + b];
-    A.s_out = (void*)(__attribute__((address_space(1))) char*)A0.tab[2 * A0.n_tab + b];
-    A.zp_out = (int8_t*)(__attribute__((address_space(1))) int8_t*)A0.tab[3 * A0.n_tab + b];
-#else
     A.w = reinterpret_cast<const uint16_t*>(A0.tab[b]);
     A.q_out = reinterpret_cast<void*>(A0.tab[A0.n_tab + b]);
     A.s_out = reinterpret_cast<void*>(A0.tab[2 * A0.n_tab + b]);
     A.zp_out = reinterpret_cast<int8_t*>(A0.tab[3 * A0.n_tab + b]);
-#endif
     b = 0;
   }
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
@@ -612,16 +591,12 @@ __device__ __forceinline__ f32x2 unpk(const uint32_t u) {
 // qparams -> quantize -> dequantize -> bf16(fl32(dq / s)); the same op sequence as
 // encode_store<KIND, FQ=true> (compressed-tensors' fake_quantize on the scaled weight, then the
 // f32 division by the column scales)
-#ifndef QZ_FQ_MAX3
-#define QZ_FQ_MAX3 1  // symmetric fake-quant: f32 |max| by v_max3 (1) or packed u16 maxima (0); A/B knob
-#endif
 template <int LOGL, int KIND, bool SYM>
 __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2* cs, const f32x2* rc, const bool cs_ok) {
   constexpr int L = 1 << LOGL;
   const uint32_t wd[4] = {v.x, v.y, v.z, v.w};
   f32x2 x[4];
   float mn, mx;
-#if QZ_FQ_MAX3
   // W * s rounded to bf16 straight into f32 lanes (bfr2: one convert per element) and the
   // group's |max| by three-input maxima with |.| source modifiers (4 VALU for 8 elements);
   // the inputs are finite (D12), so the maximum is exact and order-free
@@ -634,20 +609,6 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
     asm("v_max3_f32 %0, %1, %2, |%3|" : "=v"(m2) : "v"(m0), "v"(m1), "v"(x[3].x));
     asm("v_max_f32 %0, %1, |%2|" : "=v"(m3) : "v"(m2), "v"(x[3].y));
     mx = __uint_as_float(grp_max_u<L>(__float_as_uint(m3)));
-    mn = -mx;
-  } else
-#endif
-  if (SYM) {  // |bf16| bit patterns, two per dword
-    uint32_t xw[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      xw[k] = pk_bf16(unpk(wd[k]) * cs[k]);  // W * s in the weight dtype
-      x[k] = unpk(xw[k]);
-    }
-    const uint32_t m = pk_max_u16(pk_max_u16(xw[0] & 0x7fff7fffu, xw[1] & 0x7fff7fffu),
-                                  pk_max_u16(xw[2] & 0x7fff7fffu, xw[3] & 0x7fff7fffu));
-    const uint32_t am = grp_max_u<L>(max(m & 0xffffu, m >> 16) << 16);
-    mx = __uint_as_float(am);
     mn = -mx;
   } else {
 #pragma unroll
@@ -726,12 +687,8 @@ __device__ __forceinline__ uint4 fq_unit(const QP& p, const uint4 v, const f32x2
   return make_uint4(pk_bf16(q[0]), pk_bf16(q[1]), pk_bf16(q[2]), pk_bf16(q[3]));
 }
 
-// QZ_FQ_TILES > 1: a wave walks that many consecutive row tiles, loading tile t+1 before it
-// computes tile t (A/B knob; 1 = one tile per wave)
-#ifndef QZ_FQ_TILES
-#define QZ_FQ_TILES 1
-#endif
-constexpr int FQ_TILES = QZ_FQ_TILES;
+// one tile per wave (several consecutive tiles per wave, the next one's loads in flight,
+// measured slower: profiles/r02ay_fq_tiles_ab.log)
 
 template <bool NT, int U>
 __device__ __forceinline__ void fq_load_tile(uint4 (&v)[U], const uint4* src, int64_t r0, int64_t rows, int64_t upr,
@@ -765,9 +722,9 @@ template <int LOGL, int KIND, bool SYM, bool NT>
 __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   constexpr int U = FQ_ROWS;
   const int lane = threadIdx.x & (WAVE - 1);
-  // a block of FQ_TILES tiles (wave index through readfirstlane: wave-uniform to the compiler)
+  // this wave's tile (wave index through readfirstlane: wave-uniform to the compiler)
   const int64_t rblk = (int64_t)blockIdx.y * (FBLOCK / WAVE) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (rblk * U * FQ_TILES >= rows) return;
+  if (rblk * U >= rows) return;
   const int64_t b = blockIdx.z;
   const int64_t upr = A.units_per_row;
   const int64_t cu = (int64_t)blockIdx.x * WAVE + lane;  // this lane's column unit
@@ -778,7 +735,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   // one tile per wave: the tile's rows through one source and one destination descriptor
   // (wave-uniform bases, 32-bit lane / row offsets: no per-unit 64-bit address arithmetic); rows
   // past the slice re-read its last row and are not stored, nor are lanes past the last column
-  constexpr bool BUF = QZ_FQ_BUF && FQ_TILES == 1 && !NT;
+  constexpr bool BUF = QZ_FQ_BUF && !NT;
   uint32_t voff = 0, roff[U];
   __amdgpu_buffer_rsrc_t rs_dst;
   int nrow_b = 0;
@@ -798,7 +755,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
     for (int u = 0; u < U; ++u)
       v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], QZ_FQ_LD_AUX));
   } else {
-    fq_load_tile<NT, U>(v, src, rblk * U * FQ_TILES, rows, upr, cuc);
+    fq_load_tile<NT, U>(v, src, rblk * U, rows, upr, cuc);
   }
   // this lane's 8 column scales, their reciprocals, and whether rcp is accurate for all 8
   const float* csp = A.col_scales + b * A.cs_ld_batch + cuc * 8;
@@ -823,25 +780,14 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
     }
     return;
   }
+  const int64_t r0 = rblk * U;
+  uint4* dst = reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + r0 * upr + cuc;
+  const int nrow = (int)min<int64_t>(U, rows - r0);  // rows of this tile inside the slice
 #pragma unroll
-  for (int t = 0; t < FQ_TILES; ++t) {
-    const int64_t r0 = (rblk * FQ_TILES + t) * U;
-    if (r0 >= rows) break;  // wave-uniform
-    uint4 nv[U];
-    const bool more = t + 1 < FQ_TILES && r0 + U < rows;
-    if (more) fq_load_tile<NT, U>(nv, src, r0 + U, rows, upr, cuc);  // in flight while tile t computes
-    uint4* dst = reinterpret_cast<uint4*>(A.q_out) + b * A.units_per_batch + r0 * upr + cuc;
-    const int nrow = (int)min<int64_t>(U, rows - r0);  // rows of this tile inside the slice
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
-      if (col_ok && u < nrow) st_out<false>(dst, o);
-      dst += upr;
-    }
-    if (more) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = nv[u];
-    }
+  for (int u = 0; u < U; ++u) {
+    const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
+    if (col_ok && u < nrow) st_out<false>(dst, o);
+    dst += upr;
   }
 }
 
@@ -1723,7 +1669,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
 #ifndef QZ_FQ_COLS
 #define QZ_FQ_COLS 1  // column-tiled AWQ fake-quant kernel (0: unit-wise k_group_fast, A/B knob)
 #endif
-    const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS * FQ_TILES), FBLOCK / WAVE);
+    const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS), FBLOCK / WAVE);
     FqcFn fqc = (QZ_FQ_COLS && fq && col_scales) ? pick_fqc(logl, pl.kind, pl.p.sym != 0, nt) : nullptr;
     if (fqc && fq_yblocks <= 65535) {
       hipLaunchKernelGGL(fqc, dim3((unsigned)cdiv(F.units_per_row, WAVE), (unsigned)fq_yblocks, (unsigned)batch),
@@ -1858,11 +1804,8 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
   const bool nt = n * rows * cols * 2 > QZ_NT_BYTES_Q;
   const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(false, nt) * WAVE);
   const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
-#ifndef QZ_GRP_DYN_LDS
-#define QZ_GRP_DYN_LDS 0  // tuning knob: dynamic LDS per workgroup (caps occupancy)
-#endif
   hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, nt, true), dim3((unsigned)blocks, (unsigned)n),
-                     dim3(FBLOCK), QZ_GRP_DYN_LDS, (hipStream_t)stream, F);
+                     dim3(FBLOCK), 0, (hipStream_t)stream, F);
   return launch_err();
 }
 

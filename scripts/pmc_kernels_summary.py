@@ -31,8 +31,6 @@ KERNELS = {
     "k_scale_v8<true>": ("AWQ smoothing W[:, c] *= s[c]", P * 4 + C * 4),
     "k_absmean_1l<": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
     "k_wmean_1l<": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
-    "k_stats_dma<0": ("AWQ absmean [16384, 4096], one launch, LDS-DMA walk (round 4)", T * C * 2),
-    "k_stats_dma<1": ("AWQ w_mean [11008, 4096] g128, one launch, LDS-DMA walk (round 4)", P * 2),
     # NVFP4 [128, 768, 2048]: read 2 B + codes 0.5 B + e4m3 scale 1/16 B per param + f32 per slice
     "k_nv_encode<false>": ("NVFP4 fused encode launch, Qwen3-30B-A3B expert half [128, 768, 2048] (round 4)",
                            int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
