@@ -79,6 +79,24 @@ def test_small_slices_match_oracle(cuda):
     _sync_clean(cuda)
 
 
+def test_extreme_magnitudes_match_oracle(cuda):
+    """Slices scaled by 2^-120 .. 2^100 (global scales near the ends of the f32 range, group scales
+    whose reciprocal leaves rcp's accurate range) and a slice whose groups span 60 binades: the
+    encode's scale tables and e4m3 conversion vs the C oracle, slice by slice."""
+    a = QuantizationArgs(**NV)
+    base = _rand((6, 64, 256), seed=77, scale=1.0)
+    mult = torch.tensor([2.0 ** -120, 2.0 ** -60, 1.0, 2.0 ** 40, 2.0 ** 100, 1.0]).view(6, 1, 1)
+    w = (base.float() * mult).to(torch.bfloat16)
+    w[5] = (base[5].float() * (2.0 ** torch.arange(-30, 34, dtype=torch.float32).view(64, 1))).to(torch.bfloat16)
+    got = ops.quantize_weight(w.to(cuda), a)
+    for i in range(w.shape[0]):
+        ref = qref.compress_weight(w[i], _OA)
+        _same(got["codes"][i], ref["weight_packed"])
+        _same(got["scale"][i], ref["weight_scale"])
+        _same(got["global_scale"][i:i + 1], ref["weight_global_scale"])
+    _sync_clean(cuda)
+
+
 def test_qwen3_30b_a3b_fused_experts(cuda):
     """One Qwen3-30B-A3B MoE layer: gate_up_proj [128, 1536, 2048] as its strided gate / up halves
     (48 tiles per slice) and down_proj [128, 2048, 768]: bit-identical to the two-pass path, and
