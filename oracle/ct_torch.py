@@ -319,6 +319,7 @@ def pack_fp4_to_uint8(x: torch.Tensor) -> torch.Tensor:
     grid = torch.tensor(FP4_GRID, dtype=x.dtype)
     idx = torch.argmin(torch.abs(torch.abs(x).unsqueeze(-1) - grid), dim=-1)
     idx = idx + (torch.signbit(x).to(torch.long) << 3)
+    idx[torch.isnan(x)] = 0  # D17: a NaN's sign bit is platform-defined (x86 0/0 is negative)
     idx = idx.reshape(-1, 2)
     return (idx[:, 0] | (idx[:, 1] << 4)).to(torch.uint8).reshape(m, n // 2)
 

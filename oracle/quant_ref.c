@@ -63,6 +63,7 @@ static float e4m32f(uint8_t c) {
 /* FP4_E2M1_DATA.cast_to_fp4 thresholds, applied to |x|; returns the grid index, sign bit
  * = signbit of sign(x)*|q| (torch.sign(0) = 0 so zero stays +0, small negatives give -0). */
 static uint8_t fp4_code(float x) {
+  if (x != x) return 0; /* D17: a NaN quotient (0 / 0 under an overflowed NVFP4 global scale) */
   float a = fabsf(x);
   int idx;
   if (a <= 0.25f) idx = 0;

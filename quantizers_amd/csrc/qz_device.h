@@ -110,7 +110,7 @@ __device__ __forceinline__ float e4m3_to_f32(uint32_t c) {
 
 // ------------------------------------------------------------------ FP4 E2M1
 // FP4_E2M1_DATA.cast_to_fp4 thresholds on |x|; sign bit from sign(x) (x<0 -> 0x8, even when
-// the magnitude rounds to 0).
+// the magnitude rounds to 0).  A NaN passes no threshold test: code 0 (D17)
 __device__ __forceinline__ uint32_t fp4_code(float x) {
   float a = fabsf(x);
   uint32_t idx = (a > 0.25f) + (a >= 0.75f) + (a > 1.25f) + (a >= 1.75f) + (a > 2.5f) +

@@ -227,6 +227,13 @@ __device__ __forceinline__ uint32_t bf16_div_pk(f32x2 d, f32x2 c) {
   return pk_bf16(q);
 }
 
+// NVFP4 quotient x / s clamped to the E2M1 range, "+ 0" turning -0 into +0 (torch.sign(-0.) is
+// 0); a NaN quotient (0 / 0: a zero element of a slice whose global scale overflowed to inf)
+// encodes as code 0 whatever its sign bit (D17)
+__device__ __forceinline__ float nv_clamp(float q) {
+  return q != q ? 0.0f : __builtin_amdgcn_fmed3f(q, -6.f, 6.f) + 0.0f;
+}
+
 // quotient, round/clamp/encode and store of one 8-element unit whose group params are known.
 // unit = dense output unit index.  Returns false for invalid (out-of-range) units.
 template <int KIND, bool FQ, bool SYM, bool NTS = false>
@@ -248,8 +255,8 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       const float qa = x[k].x * g.rs, qb = x[k].y * g.rs;
       const bool near = min((__float_as_uint(qa) << 11) + 0x2000u, (__float_as_uint(qb) << 11) + 0x2000u) < 0x4000u;
       if (__builtin_expect(near || !g.fast, 0)) {
-        ca[k] = __builtin_amdgcn_fmed3f(x[k].x / g.s, -6.f, 6.f) + 0.0f;
-        cb[k] = __builtin_amdgcn_fmed3f(x[k].y / g.s, -6.f, 6.f) + 0.0f;
+        ca[k] = nv_clamp(x[k].x / g.s);
+        cb[k] = nv_clamp(x[k].y / g.s);
       } else {
         ca[k] = __builtin_amdgcn_fmed3f(qa, -6.f, 6.f);
         cb[k] = __builtin_amdgcn_fmed3f(qb, -6.f, 6.f);
@@ -350,9 +357,9 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         // v_cvt_scalef32_pk_fp4_f32: RNE on the E2M1 grid == cast_to_fp4's thresholds (checked
         // exhaustively); "+ 0" maps an exact -0 input to +0 (torch.sign(-0.) is 0 -> code 0),
         // small negatives still round to -0 (code 8) as sign(x)*|q| does
-        const uint32_t pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(
-            0u, __builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f) + 0.0f, __builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f) + 0.0f,
-            1.0f, 0);
+        const float ca = KIND == K_NV ? nv_clamp(t[k].x) : __builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f) + 0.0f;
+        const float cb = KIND == K_NV ? nv_clamp(t[k].y) : __builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f) + 0.0f;
+        const uint32_t pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, ca, cb, 1.0f, 0);
         c[2 * k] = pk & 0xfu;
         c[2 * k + 1] = (pk >> 4) & 0xfu;
       } else {

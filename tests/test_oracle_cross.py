@@ -48,3 +48,20 @@ def test_fused_c_leg_matches():
         r = ct.compress_weight(w, ct.QArgs(group_size=gs))
         _eq(p, r["weight_packed"])
         _eq(s, r["weight_scale"])
+
+
+def test_fp4_nan_code():
+    """D17: an NVFP4 slice whose |w| maximum is so small that its global scale overflows to inf
+    divides its zero elements 0 / 0; both restatements encode that NaN as code 0 (of either sign
+    of zero), and agree on the rest of the slice."""
+    g = torch.Generator().manual_seed(3)
+    w = (torch.randn(16, 64, generator=g) * 2.0 ** -122).to(torch.bfloat16)
+    w[0, :4] = 0.0
+    w[1, :4] = -0.0
+    a = ct.QArgs(num_bits=4, type="float", group_size=16, strategy="tensor_group", scale_dtype="fp8")
+    r1, r2 = ct.compress_weight(w, a), qref.compress_weight(w, a)
+    assert torch.isinf(r1["weight_global_scale"]).all()
+    for k, v in r1.items():
+        _eq(v, r2[k])
+    codes = r1["weight_packed"]
+    assert (codes[0, :2] == 0).all() and (codes[1, :2] == 0).all()
