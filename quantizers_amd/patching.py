@@ -6,6 +6,7 @@ from __future__ import annotations
 import contextlib
 import dis
 import logging
+import os
 from typing import Callable, List, Tuple
 
 import torch
@@ -72,10 +73,17 @@ def _per_batch_mm(a, b):
     return out.reshape(*lead, a.shape[-2], b.shape[-1])
 
 
+BMM_GUARD = os.environ.get("QZ_BMM_GUARD", "1") == "1"
+
+
 @contextlib.contextmanager
 def bmm_guard():
     """torch.bmm / torch.matmul / Tensor.matmul / Tensor.__matmul__ with the pinned defect's
-    operands go through ``_per_batch_mm`` inside the context; everything else is untouched."""
+    operands go through ``_per_batch_mm`` inside the context; everything else is untouched.
+    ``QZ_BMM_GUARD=0`` leaves torch as it is (A/B knob)."""
+    if not BMM_GUARD:
+        yield
+        return
     saved = (torch.bmm, torch.matmul, torch.Tensor.matmul, torch.Tensor.__matmul__)
 
     def wrap(orig):
