@@ -159,7 +159,8 @@ int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* row
 /*
  * qz_quantize_nvfp4 / qz_quantize_grouped_nvfp4 -- NVFP4 (TENSOR_GROUP, FP4 E2M1, group 16, e4m3
  * group scales, f32 per-slice global scale) in TWO launches and no workspace fills.  Replaces the
- * same observer -> calculate_qparams -> quantize -> pack_fp4_to_uint8 chain as qz_quantize for the
+ * same observer -> calculate_qparams -> quantize -> pack_fp4_to_uint8 chain as qz_quantize
+ * (oneshot, scripts/do_oneshot.py:179-187; save_pretrained(save_compressed=True), :197) for the
  * reference's NVFP4 recipes (configs/recipes/recipe_MoE_RTN_NVFP4.yaml:16-21,
  * recipe_Dense_NVFP4.yaml:7-12; scheme preset NVFP4), with results identical to qz_quantize's.
  * The first launch reduces every slice's |w| maximum into `sync`, the second encodes (each slice
