@@ -207,7 +207,8 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
     -> NVFP4: E2M1 codes, e4m3 group-16 scales, one f32 global scale per expert linear): every
     expert weight of the 48 layers (4 resident fused layers rotated, as the MXFP4 leg) through
     the fused NVFP4 path (qz_quantize_nvfp4 -> k_nv_absmax + k_nv_encode, two launches per fused
-    parameter, no fills), outputs preallocated.  HIP events on the launch stream around one whole
+    parameter, no fills; the parameters round-robin over 2 streams as CompressionPlan issues them,
+    ops.quantize_nvfp4_many; one stream reported beside it), outputs preallocated.  HIP events on the launch stream around one whole
     pass (288 launches back to back); the generic qz_quantize path (absmax pre-pass, global-scale
     launch, group kernel: five launches) timed the same way beside it.  Algorithmic bytes per
     param = 2.5625 (+ 4 B per expert linear); the path reads every weight twice (the global
@@ -224,10 +225,13 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
     ws = torch.empty(lib.qz_quantize_workspace_size(128, 2048, 768, ctypes.byref(ca)) + 256, dtype=torch.uint8,
                      device=dev)
 
-    def fused():
-        for li in range(48):
-            for lj, j, w in views[(li % 4) * 3:(li % 4) * 3 + 3]:
-                ops.quantize_weight(w, nv, out=outs[(lj, j)])
+    items = [(w, outs[(lj, j)]) for li in range(48) for lj, j, w in views[(li % 4) * 3:(li % 4) * 3 + 3]]
+
+    def fused():  # as CompressionPlan issues NVFP4 parameters: round-robin over 2 streams
+        ops.quantize_nvfp4_many(items, nv)
+
+    def fused_one_stream():
+        ops.quantize_nvfp4_many(items, nv, n_streams=1)
 
     def two_pass():
         for li in range(48):
@@ -244,7 +248,7 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
            "recipe": "reference configs/recipes/recipe_MoE_RTN_NVFP4.yaml (scheme NVFP4)",
            "timing": "HIP events around one whole pass (144 fused parameters back to back), best of 3"}
     st = torch.cuda.current_stream(dev)
-    for name, fn in (("fused", fused), ("two_pass", two_pass)):
+    for name, fn in (("fused", fused), ("fused_one_stream", fused_one_stream), ("two_pass", two_pass)):
         fn()
         torch.cuda.synchronize()
         best = None
@@ -261,6 +265,8 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
                "streamed_frac": (npar * (NV_B_PER_PARAM + 2) + 48 * 3 * 128 * 4) / best / 1e9 / HBM_PEAK_GBS}
         if name == "fused":
             res.update(leg)
+        elif name == "fused_one_stream":
+            res["one_stream"] = leg
         else:
             res["two_pass_qz_quantize"] = leg
     del outs

@@ -226,9 +226,18 @@ class CompressionPlan:
         for gq, *_ in self.grouped:  # one stream: spreading the launches over 2-3 streams measured
             gq.run(main)             # slower (r02r A/B)
         if self.singles:
-            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream(self.device)):
+            nv = [(w, o, a) for u, w, o, a, int_q, fmt in self.singles if a.is_nvfp4 and fmt == ops.default_out_fmt(a)]
+            with torch.cuda.stream(main):
                 for u, w, o, a, int_q, fmt in self.singles:
-                    ops.quantize_weight(w, a, out_fmt=fmt, out=o)
+                    if not (a.is_nvfp4 and fmt == ops.default_out_fmt(a)):
+                        ops.quantize_weight(w, a, out_fmt=fmt, out=o)
+            # NVFP4 parameters (stacked fused experts): two streams, one's |w| max launch beside
+            # the other's encode (ops.quantize_nvfp4_many); grouped by scheme
+            by_args: Dict[int, list] = {}
+            for w, o, a in nv:
+                by_args.setdefault(id(a), [a, []])[1].append((w, o))
+            for a, items in by_args.values():
+                ops.quantize_nvfp4_many(items, a, stream=main)
 
     def tensors(self) -> Dict[str, torch.Tensor]:
         """The on-disk tensors of every unit (device tensors; ``weight_shape`` on the host)."""

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""NVFP4 experts pass (48 layers x 3 fused expert parameters, 4 resident layers rotated) issued on
+1 stream vs alternating over 2 / 3 streams (each with its own sync region), so one parameter's
+|w| max launch (HBM-read-bound) can run beside the previous one's encode launch.  HIP events on
+the default stream around the whole pass (the side streams joined).  Bit-identical outputs are
+checked against the 1-stream pass.  Usage: python scripts/nv_streams_probe.py"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from quantizers_amd import ops  # noqa: E402
+from quantizers_amd.quantization import QuantizationArgs  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    a = QuantizationArgs(num_bits=4, type="float", strategy="tensor_group", group_size=16, scale_dtype="float8_e4m3fn")
+    g = torch.Generator(device=dev).manual_seed(0)
+    layers = [((torch.randn(128, 1536, 2048, device=dev, generator=g) * 0.02).to(torch.bfloat16),
+               (torch.randn(128, 2048, 768, device=dev, generator=g) * 0.02).to(torch.bfloat16)) for _ in range(4)]
+    views = [w for gu, dn in layers for w in (gu[:, :768], gu[:, 768:], dn)]
+    outs = [ops.alloc_outputs(tuple(w.shape), a, None, dev) for w in views]
+    main_st = torch.cuda.current_stream(dev)
+    npar = 48 * 128 * 3 * 768 * 2048
+    nb = npar * (2 + 0.5 + 1 / 16)
+    ref = None
+    for ns in (1, 2, 3, 1, 2, 3):
+        sts = [main_st] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+
+        def run():
+            for s in sts[1:]:
+                s.wait_stream(main_st)
+            for i in range(48 * 3):
+                s = sts[i % ns]
+                with torch.cuda.stream(s):
+                    ops.quantize_weight(views[i % 12], a, out=outs[i % 12])
+            for s in sts[1:]:
+                main_st.wait_stream(s)
+        run()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(main_st)
+            run()
+            e1.record(main_st)
+            torch.cuda.synchronize()
+            t = e0.elapsed_time(e1) * 1e-3
+            best = t if best is None else min(best, t)
+        got = [o["codes"].clone() for o in outs]
+        same = ref is None or all(torch.equal(x, y) for x, y in zip(ref, got))
+        ref = ref or got
+        print(json.dumps({"streams": ns, "ms": best * 1e3, "frac": nb / best / 1e9 / 8000, "same_codes": same}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

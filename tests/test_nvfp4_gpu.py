@@ -187,3 +187,23 @@ def test_argument_errors(cuda):
     assert lib.qz_quantize_nvfp4(*args(mx.to_c())) == _lib.QZ_ERR_FORMAT
     assert lib.qz_quantize_nvfp4(*args(a.to_c())) == 0
     torch.cuda.synchronize()
+
+
+def test_many_on_two_streams(cuda):
+    """ops.quantize_nvfp4_many (round-robin over 2 streams, as CompressionPlan issues NVFP4
+    parameters) == one quantize_weight call per parameter on one stream, and a following
+    default-stream read sees every output."""
+    a = QuantizationArgs(**NV)
+    gu = _rand((16, 512, 1024), seed=61, device=cuda)
+    dn = _rand((16, 1024, 256), seed=62, device=cuda)
+    ws = [gu[:, :256], gu[:, 256:], dn, gu[:, :256] * 3]
+    refs = [ops.quantize_weight(w, a) for w in ws]
+    outs = [ops.alloc_outputs(tuple(w.shape), a, None, cuda) for w in ws]
+    for o in outs:
+        for t in o.values():
+            if t is not None:
+                t.fill_(0) if t.dtype != torch.float8_e4m3fn else t.view(torch.uint8).fill_(0)
+    ops.quantize_nvfp4_many(list(zip(ws, outs)), a, n_streams=2)
+    for o, r in zip(outs, refs):  # read on the default stream right after (no synchronize)
+        for k in ("codes", "scale", "global_scale"):
+            _same(o[k], r[k])
