@@ -224,7 +224,14 @@ class CompressionPlan:
         if self._ready is not None:
             main.wait_event(self._ready)
         for gq, *_ in self.grouped:  # one stream: spreading the launches over 2-3 streams measured
-            gq.run(main)             # slower (r02r A/B)
+            if not gq.nvfp4:         # slower (r02r A/B) -- except NVFP4's two-launch calls:
+                gq.run(main)
+        nvg = [gq for gq, *_ in self.grouped if gq.nvfp4]
+        if nvg:  # Qwen3-4B NVFP4, 7 calls: 3.14-3.18 -> 2.95-2.96 ms on 2 streams (r04y_nv_streams_dense.log)
+            sts = ops.nvfp4_streams(self.device, main)
+            for i, gq in enumerate(nvg):
+                gq.run(sts[i % len(sts)])
+            ops.join_streams(sts)
         if self.singles:
             nv = [(w, o, a) for u, w, o, a, int_q, fmt in self.singles if a.is_nvfp4 and fmt == ops.default_out_fmt(a)]
             with torch.cuda.stream(main):

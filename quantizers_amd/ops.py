@@ -364,31 +364,44 @@ NVFP4_STREAMS = int(os.environ.get("QZ_NVFP4_STREAMS", "2"))
 _side_streams: Dict[Tuple[int, int, int], torch.cuda.Stream] = {}
 
 
-def quantize_nvfp4_many(items: Sequence[Tuple[torch.Tensor, Dict[str, torch.Tensor]]], a: QuantizationArgs,
-                        stream=None, n_streams: Optional[int] = None) -> None:
-    """``quantize_weight(w, a, out=o)`` for every (w, o) of NVFP4 items, issued round-robin over
-    ``n_streams`` streams (the caller's stream first; the side streams join it at the end, each
-    with its own sync region): one parameter's |w| max launch, bound by HBM reads, runs beside the
-    previous one's encode launch.  Qwen3-30B-A3B experts pass 21.2-21.3 -> 20.2-20.3 ms on 2
-    streams, 3 streams 21.0 ms, outputs identical (profiles/r04w_nv_streams_probe.log)."""
-    if not items:
-        return
-    ns = max(1, NVFP4_STREAMS if n_streams is None else n_streams)
-    dev = items[0][0].device
+def nvfp4_streams(device, stream=None, n_streams: Optional[int] = None) -> List[torch.cuda.Stream]:
+    """The streams NVFP4 work is spread over: the caller's stream first, then ``n_streams - 1``
+    side streams (cached per caller stream) that wait for it; ``join_streams`` makes the caller's
+    stream wait for them.  Two streams let one NVFP4 call's |w| max launch (read-bound) run beside
+    the previous call's encode launch (VALU-heavy)."""
+    dev = torch.device(device)
     main = stream if stream is not None else torch.cuda.current_stream(dev)
     sts = [main]
-    for k in range(1, ns):
+    for k in range(1, max(1, NVFP4_STREAMS if n_streams is None else n_streams)):
         key = (dev.index or 0, main.cuda_stream, k)
         if key not in _side_streams:
             _side_streams[key] = torch.cuda.Stream(dev)
         sts.append(_side_streams[key])
     for s in sts[1:]:
         s.wait_stream(main)
+    return sts
+
+
+def join_streams(sts: List[torch.cuda.Stream]) -> None:
+    """The first stream waits for the others: later work on it -- and any reuse of the memory the
+    side streams touched through it -- is ordered after theirs."""
+    for s in sts[1:]:
+        sts[0].wait_stream(s)
+
+
+def quantize_nvfp4_many(items: Sequence[Tuple[torch.Tensor, Dict[str, torch.Tensor]]], a: QuantizationArgs,
+                        stream=None, n_streams: Optional[int] = None) -> None:
+    """``quantize_weight(w, a, out=o)`` for every (w, o) of NVFP4 items, round-robin over
+    ``nvfp4_streams`` (each stream with its own sync region).  Qwen3-30B-A3B experts pass
+    21.2-21.3 -> 20.2-20.3 ms on 2 streams, 3 streams 21.0 ms, outputs identical
+    (profiles/r04w_nv_streams_probe.log)."""
+    if not items:
+        return
+    sts = nvfp4_streams(items[0][0].device, stream, n_streams)
     for i, (w, o) in enumerate(items):
-        with torch.cuda.stream(sts[i % ns]):
+        with torch.cuda.stream(sts[i % len(sts)]):
             quantize_weight(w, a, out=o)
-    for s in sts[1:]:  # the caller's stream waits for every side stream: later work on it (and any
-        main.wait_stream(s)  # reuse of these tensors' memory through it) is ordered after them
+    join_streams(sts)
 
 
 def fake_quantize(w: torch.Tensor, a: QuantizationArgs, col_scales: Optional[torch.Tensor] = None,

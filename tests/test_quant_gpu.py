@@ -790,6 +790,42 @@ def test_whole_model_plan_equals_per_weight(cuda):
     torch.cuda.empty_cache()
 
 
+def test_whole_model_plan_nvfp4_two_streams(cuda):
+    """recipe_Dense_NVFP4 on the Qwen3-4B model: the CompressionPlan's 7 grouped NVFP4 calls, run
+    over two streams (ops.nvfp4_streams), give every on-disk tensor bit-identical to the per-weight
+    call; one weight per shape also vs the plain-C oracle."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import qref
+    from quantizers_amd.compressor import CompressionPlan, compression_units
+    from quantizers_amd.quantization import preset_scheme
+    torch.manual_seed(4)
+    model = bench.build_model(cuda)
+    nv = preset_scheme("NVFP4", ["Linear"])
+    model.quantization_scheme_map = {n: nv for n in model.quantization_scheme_map}
+    units, _ = compression_units(model)
+    plan = CompressionPlan(units, cuda)
+    assert sum(1 for gq, *_ in plan.grouped if gq.nvfp4) == 5 and len(units) == 252
+    plan.run()
+    got = plan.tensors()
+    seen = set()
+    for u in units:
+        w = u.refs[0].weight
+        ref = ops.compress_weight(w, u.scheme.weights)
+        for k, v in ref.items():
+            _eq(got[f"{u.refs[0].name}.{k}"], v)
+        if tuple(w.shape) not in seen:
+            seen.add(tuple(w.shape))
+            want = qref.compress_weight(w.cpu(), _oracle_args(u.scheme.weights))
+            for k, v in want.items():
+                if not k.startswith("_"):
+                    _eq(got[f"{u.refs[0].name}.{k}"], v)
+    del model, plan, got
+    torch.cuda.empty_cache()
+
+
 def test_stats_one_launch_stress_many_grids(cuda):
     """the one-launch statistics reductions hand partials between workgroups through
     agent-coherent stores / loads and counters (no release / acquire fence).  Over 24 grid shapes
