@@ -6,7 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r04q}
 export TMPDIR=/tmp
-TESTS="tests/test_nvfp4_gpu.py" SKIP_BENCH=0 PROFILE=1 TAG=$TAG bash scripts/gpu_session.sh || exit $?
+TESTS="${TESTS:-tests/test_nvfp4_gpu.py}" SKIP_BENCH=0 PROFILE=1 TAG=$TAG bash scripts/gpu_session.sh || exit $?
 TAG=$TAG bash scripts/pmc_kernels.sh || exit $?
 TAG=$TAG bash scripts/pmc_headline.sh || exit $?
 echo evidence done
