@@ -25,6 +25,7 @@ def main(n=30):
     copies = [(torch.randn(R, C, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for _ in range(12)]
     a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=G)
     s = torch.rand(C, device=dev, generator=gen) + 0.5
+    grid_s = [torch.rand(C, device=dev, generator=gen) + 0.5 for _ in range(20)]
     fq_out = [torch.empty_like(copies[0]) for _ in range(4)]
     x = [torch.randn(16384, C, device=dev, generator=gen).to(torch.bfloat16) for _ in range(4)]
     sums = torch.zeros(C, dtype=torch.float32, device=dev)
@@ -36,6 +37,9 @@ def main(n=30):
     kernels = [
         ("quantize_per_weight", lambda i: prep.run(copies[i % 12]), 1),
         ("fake_quant_cols", lambda i: ops.fake_quantize(copies[i % 12], a, col_scales=s, out=fq_out[i % 4]), 1),
+        # the AWQ dense grid's pattern (awq._grid_fixed): ONE weight fake-quantized under 20 scale
+        # vectors into the same output (the balance layer's own weight)
+        ("fake_quant_grid", lambda i: ops.fake_quantize(copies[0], a, col_scales=grid_s[i % 20], out=fq_out[0]), 1),
         ("absmean", lambda i: ops.awq_absmean_accum(x[i % 4], sums), 1),
         ("weight_mean", lambda i: ops.awq_weight_mean_accum(copies[i % 12], G, wsum), 1),
         ("scale_columns", lambda i: ops.scale_columns_(copies[i % 12], s), 1),

@@ -19,11 +19,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 R, C = 11008, 4096
 P = R * C
 T = 16384  # activation tokens of the absmean leg (scripts/kernel_driver.py)
+LEG_LAUNCHES = 33  # per leg: 3 warm-up launches + N = 30 timed ones (scripts/pmc_kernels.sh N)
 # kernel-name substring -> (label, algorithmic bytes per launch)
 KERNELS = {
     "k_group_fast<4, 0, false, true, true, false>": ("quantize int4 g128 (per-weight launch)", int(P * 2.515625)),
     "k_group_fast<4, 0, true, true, false, false>": ("AWQ fake-quant Q(W*s)/s int4 g128 (unit-wise, r02c)", P * 4 + C * 4),
-    "k_fq_cols<4, 0, true, false>": ("AWQ fake-quant Q(W*s)/s int4 g128", P * 4 + C * 4),
+    # kernel_driver runs k_fq_cols in two legs, in this order: "#0" = 12 rotating weights into 4
+    # rotating outputs (an isolated op, cold), "#1" = the AWQ grid's pattern (one weight, 20 scale
+    # vectors, one output)
+    "k_fq_cols<4, 0, true, false>#0": ("AWQ fake-quant Q(W*s)/s int4 g128", P * 4 + C * 4),
+    "k_fq_cols<4, 0, true, false>#1": ("AWQ fake-quant Q(W*s)/s int4 g128, AWQ grid pattern (one weight, 20 scales)",
+                                       P * 4 + C * 4),
     "k_absmean_partial_v8": ("AWQ absmean stage 1 [16384, 4096]", T * C * 2),
     "k_colsum_final<float>": ("AWQ absmean stage 2", None),
     "k_wmean_v8": ("AWQ w_mean stage 1", P * 2),
@@ -56,8 +62,13 @@ def main(tag):
             w.writerow(dict(r, Name=_short(r["Name"])))
     trace = list(csv.DictReader(open(os.path.join(src, "trace", "run_kernel_trace.csv"))))
     res = {}
-    for sub, (label, alg) in KERNELS.items():
-        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace if sub in r["Kernel_Name"]]
+    def leg(rows, part):  # "#k": the k-th block of LEG_LAUNCHES consecutive launches of the kernel
+        return rows if part is None else rows[part * LEG_LAUNCHES:(part + 1) * LEG_LAUNCHES]
+    for key, (label, alg) in KERNELS.items():
+        sub, _, part = key.partition("#")
+        part = int(part) if part else None
+        mine = sorted((r for r in trace if sub in r["Kernel_Name"]), key=lambda r: int(r["Dispatch_Id"]))
+        durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in leg(mine, part)]
         if not durs:
             continue
         d = {"label": label, "launches": len(durs), "median_ns": statistics.median(durs),
@@ -67,8 +78,12 @@ def main(tag):
             if pdir == "trace" or not os.path.exists(p):
                 continue
             by = {}
-            for r in csv.DictReader(open(p)):
-                if sub in r["Kernel_Name"]:
+            rows = [r for r in csv.DictReader(open(p)) if sub in r["Kernel_Name"]]
+            seen = sorted({int(r["Dispatch_Id"]) for r in rows})  # dispatches in order
+            seen = [str(d) for d in seen]
+            keep = set(leg(seen, part))
+            for r in rows:
+                if r["Dispatch_Id"] in keep:
                     by.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
             for c, v in by.items():
                 d["counters"][c] = statistics.median(v)

@@ -32,7 +32,8 @@ def awq_main(paths, libs):
     dev = torch.device("cuda:0")
     ws = [(torch.randn(ROWS, COLS, device=dev) * 0.02).to(torch.bfloat16) for _ in range(COPIES)]
     s = (torch.rand(COLS, device=dev) + 0.5).float()
-    out = torch.empty_like(ws[0])
+    outs = [torch.empty_like(ws[0]) for _ in range(int(os.environ.get("OUTS", 1)))]  # OUTS=4: outputs beyond the MALL
+    out = outs[0]
     a = _lib.QzArgs(4, 0, 1, 2, G, 0, 0, 0)
     for lib in libs:
         lib.qz_awq_fake_quant.argtypes = [P, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
@@ -45,7 +46,8 @@ def awq_main(paths, libs):
     ops = {
         "fake_quant": (lambda lib, i: lib.qz_awq_fake_quant(P(ws[i % COPIES].data_ptr()), 1, ROWS, COLS, COLS,
                                                             ROWS * COLS, ctypes.byref(a), P(s.data_ptr()),
-                                                            P(out.data_ptr()), P(wsp.data_ptr()), wsp.numel(), sp),
+                                                            P(outs[i % len(outs)].data_ptr()), P(wsp.data_ptr()),
+                                                            wsp.numel(), sp),
                        ROWS * COLS * 4),
         "scale_columns": (lambda lib, i: lib.qz_scale_columns(P(ws[i % COPIES].data_ptr()), ROWS, COLS, COLS,
                                                               P(s.data_ptr()), i & 1, sp), ROWS * COLS * 4),
