@@ -62,7 +62,11 @@ def main(n=30):
                              ops._ptr(nv_out["codes"]), ops._ptr(nv_out["scale"]), ops._ptr(None),
                              ops._ptr(nv_out["global_scale"]), ops._ptr(nv_ws), nv_ws.numel(), ops._stream())
         _lib.check(rc, "qz_quantize")
+    # MXFP4 (BASELINE.json configs[3]): the same fused expert halves, E2M1 codes + E8M0 scales, g32
+    mx = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
+    mx_out = ops.alloc_outputs((128, 768, 2048), mx, None, dev)
     kernels += [
+        ("mxfp4_experts", lambda i: ops.quantize_weight(gus[i % 4][:, 768:], mx, out=mx_out), 1),
         ("nvfp4_fused", lambda i: ops.quantize_weight(gus[i % 4][:, :768], nv, out=nv_out), 1),
         ("nvfp4_two_pass", nv_two_pass, 1),
     ]

@@ -37,6 +37,9 @@ KERNELS = {
     "k_scale_v8<true>": ("AWQ smoothing W[:, c] *= s[c]", P * 4 + C * 4),
     "k_absmean_1l<": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
     "k_wmean_1l<": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
+    # MXFP4 [128, 768, 2048] (BASELINE configs[3]): read 2 B + codes 0.5 B + e8m0 scale 1/32 B per param
+    "k_group_fast<2, 2, false, true, true, false>": ("MXFP4 Qwen3-30B-A3B expert half [128, 768, 2048] (one launch)",
+                                                     int(128 * 768 * 2048 * (2 + 0.5 + 1 / 32))),
     # NVFP4 [128, 768, 2048]: read 2 B + codes 0.5 B + e4m3 scale 1/16 B per param + f32 per slice
     "k_nv_encode<false>": ("NVFP4 fused encode launch, Qwen3-30B-A3B expert half [128, 768, 2048] (round 4)",
                            int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
