@@ -173,7 +173,8 @@ static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics
 #define QZ_ABS1_WPB 8
 #endif
 #ifndef QZ_ABS1_NB
-#define QZ_ABS1_NB 8
+#define QZ_ABS1_NB 16  // rows per lane per walk batch ([16384, 4096]: a whole 512-token chunk in flight;
+                        // 24.79 -> 24.35 us back to back, same bits: profiles/r04aj_tune_stats.log)
 #endif
 #ifndef QZ_ABS1_BLOCKS
 #define QZ_ABS1_BLOCKS 1024  // tuning knob: target workgroups of the one-launch absmean
