@@ -58,6 +58,8 @@ ALG_BYTES = PARAMS * 2 + PARAMS * BITS // 8 + (PARAMS // GROUP) * 2  # 113,426,4
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "params quantized/sec + achieved HBM GB/s, Qwen3-4B AWQ int4-g128"
 RECIPE = os.path.join(ROOT, "configs", "recipes", "awq_w4a16_g128.yaml")
+# BASELINE.json configs[2]: FP8_BLOCK attention + int4 g32 MLP (reference recipe_mixed_fp8_int4.yaml, M1 corrected)
+MIXED_RECIPE = os.path.join(ROOT, "configs", "recipes", "mixed_fp8_block_awq_int4.yaml")
 MODEL_CFG = os.path.join(ROOT, "configs", "models", "qwen3-4b")
 
 # Qwen3-4B linear shapes (hidden 2560, inter 9728, 32 q / 8 kv heads x 128), 36 layers
@@ -159,20 +161,60 @@ def _timed(fn, reps=3):
     return (time.perf_counter() - t0) / reps
 
 
-def other_configs(ops, QuantizationArgs, dev, gen):
-    """BASELINE.json configs[2] (Qwen3-4B FP8_BLOCK attention + int4-g32 MLP) and configs[3]
-    (Qwen3-30B-A3B experts -> MXFP4): one quantize pass over every targeted weight."""
-    res = {}
-    fp8b = QuantizationArgs(num_bits=8, type="float", strategy="block", block_structure=[128, 128])
-    i4 = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
-    ws = [(fp8b if n.endswith(("q_proj", "k_proj", "v_proj", "o_proj")) else i4,
-           (torch.randn(QWEN3_LAYERS, r, c, device=dev, generator=gen) * 0.02).to(torch.bfloat16))
-          for n, r, c in QWEN3_4B]
-    npar = sum(w.numel() for _, w in ws)
-    t = _timed(lambda: [ops.quantize_weight(w, a) for a, w in ws])
-    res["qwen3_4b_mixed_fp8block_int4g32"] = {"params": npar, "ms": t * 1e3, "params_per_s": npar / t}
-    del ws
+def mixed_plan_leg(ops, dev, stream, steps=10):
+    """BASELINE.json configs[2] through the product: the Qwen3-4B model (public dims, random bf16)
+    under the mixed recipe (configs/recipes/mixed_fp8_block_awq_int4.yaml = the reference's
+    recipe_mixed_fp8_int4.yaml with quirk M1 corrected: FP8_BLOCK on q/k/v/o, int4 sym g32 on
+    gate/up/down), compressed by ``compressor.CompressionPlan`` exactly as ``save_compressed`` runs
+    it: 5 grouped launches per step (q, k+v, o through the FP8_BLOCK strip kernel; gate+up, down
+    through the group kernel).  HIP events on the launch stream around ``steps`` whole steps;
+    algorithmic bytes = every weight read once + every output written once (plan.alg_bytes());
+    per-launch figures from one event pair per launch."""
+    from quantizers_amd.compressor import CompressionPlan, compression_units
+    torch.manual_seed(1235)
+    model = build_model(dev, MIXED_RECIPE)
+    units, _ = compression_units(model)
+    plan = CompressionPlan(units, dev)
+    for _ in range(3):
+        plan.run(stream)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        plan.run(stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    s = e0.elapsed_time(e1) * 1e-3 / steps
+    alg = plan.alg_bytes()
+    per = []
+    for gq, part, *_ in plan.grouped:
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        gq.run(stream)
+        f1.record(stream)
+        torch.cuda.synchronize()
+        us = f0.elapsed_time(f1) * 1e3
+        rb = sum(w.numel() * 2 for _, w in part)
+        nb = rb + sum(t.numel() * t.element_size() for o in gq.outs for t in o.values() if t is not None)
+        per.append({"scheme": "FP8_BLOCK 128x128" if ops.is_fp8_block128(gq.a) else
+                    f"int{gq.a.num_bits} g{gq.a.group_size}", "shape": f"{gq.rows}x{gq.cols}", "weights": gq.n,
+                    "us": us, "alg_bytes": nb, "frac": nb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                    "read_frac": rb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS})
+    res = {"params": plan.params, "launches_per_step": plan.launches, "ms": s * 1e3, "params_per_s": plan.params / s,
+           "alg_bytes": alg, "alg_GBps": alg / s / 1e9, "frac": alg / s / 1e9 / HBM_PEAK_GBS,
+           "read_frac": plan.params * 2 / s / 1e9 / HBM_PEAK_GBS, "per_launch": per,
+           "recipe": "configs/recipes/mixed_fp8_block_awq_int4.yaml",
+           "timing": f"HIP events on the launch stream around {steps} CompressionPlan steps"}
+    del plan, units, model
     torch.cuda.empty_cache()
+    return res
+
+
+def other_configs(ops, QuantizationArgs, dev, gen, stream):
+    """BASELINE.json configs[2] (Qwen3-4B FP8_BLOCK attention + int4-g32 MLP, through the product's
+    CompressionPlan) and configs[3] (Qwen3-30B-A3B experts -> MXFP4 / NVFP4): one quantize pass
+    over every targeted weight."""
+    res = {"qwen3_4b_mixed_fp8block_int4g32": mixed_plan_leg(ops, dev, stream)}
     # Qwen3-30B-A3B: 48 layers x 128 experts x {gate, up [768, 2048], down [2048, 768]}; 4 resident
     # layers (fused [E, 2I, H] / [E, H, I] parameters, gate/up as strided views) rotated over 48
     mx = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
@@ -442,17 +484,17 @@ def awq_oneshot_layers(dev, n_layers=3, n_seq=16, seq=2048):
             "recipe": "configs/recipes/awq_w4a16_g128.yaml"}
 
 
-def build_model(dev):
+def build_model(dev, recipe=RECIPE):
     """A Qwen3-4B-shaped causal LM (configs/models/qwen3-4b: public dims, 36 layers) with random
-    bf16 weights on ``dev``, its targeted modules resolved from the AWQ int4-g128 recipe exactly
-    as ``oneshot`` resolves them."""
+    bf16 weights on ``dev``, its targeted modules resolved from ``recipe`` (default: the AWQ
+    int4-g128 recipe) exactly as ``oneshot`` resolves them."""
     from transformers import AutoConfig, AutoModelForCausalLM
     from quantizers_amd.oneshot import resolve_schemes
     from quantizers_amd.recipe import parse_recipe
     cfg = AutoConfig.from_pretrained(MODEL_CFG)
     with torch.device(dev):
         model = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)
-    schemes = resolve_schemes(model, parse_recipe(RECIPE))
+    schemes = resolve_schemes(model, parse_recipe(recipe))
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}
     return model
 
@@ -862,7 +904,7 @@ def main():
         torch.cuda.empty_cache()
         if world == 1:
             extras["awq_oneshot_qwen3_4b"] = awq_oneshot_layers(dev)
-        other = other_configs(ops, QuantizationArgs, dev, gen)
+        other = other_configs(ops, QuantizationArgs, dev, gen, stream)
         other["minimax_m2_1_mixedprec_sharded"] = minimax_pass(ops, QuantizationArgs, dev, gen, world, rank)
         extras["other_configs"] = other
 

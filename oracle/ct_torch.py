@@ -407,3 +407,63 @@ def awq_fake_quant_scaled(w: torch.Tensor, s: torch.Tensor, a: QArgs) -> torch.T
     scale, zp = calculate_qparams(mn, mx, a, global_scale=gs)
     fq = fake_quantize(ws, scale, zp, a, global_scale=gs)
     return (fq.float() / s.float().view(1, -1)).to(w.dtype)
+
+
+# ----------------------------------------------------------------------------------------
+# D8, the literal reading of SURVEY A.6 ("accumulation dtype = activation dtype"): every AWQ
+# statistic, grid scale and scaled weight in the weight / activation dtype (bf16), the loss an f32
+# sum per calibration batch.  Not the oracle's decision (awq_* above): used only to MEASURE what
+# that decision changes (tests/golden/d8_probe.py).  Op order as llmcompressor's
+# _accumulate_mean / _compute_layer_means / _compute_best_scale / _compute_loss ([3P], unpinned).
+# ----------------------------------------------------------------------------------------
+def awq_accumulate_mean_literal(x: torch.Tensor, prev=None):
+    """Running mean of |x| over tokens in x's dtype: (prev_mean * prev_n + sum) / (prev_n + n),
+    every op rounded to bf16 (the per-batch sum accumulates in f32 inside torch, rounded once)."""
+    inp = x.reshape(-1, x.shape[-1]).abs()
+    s = inp.sum(0)
+    n = inp.shape[0]
+    if prev is None:
+        return s / n, n
+    pm, pc = prev
+    return (pm * pc + s) / (pc + n), pc + n
+
+
+def awq_layer_means_literal(weights, a: QArgs) -> torch.Tensor:
+    """w_mean in the weight dtype: per layer a bf16 column sum, summed across layers in bf16,
+    divided by the row count in bf16."""
+    total = 0
+    acc = None
+    for w in weights:
+        n, k = w.shape
+        g = {"tensor": w.numel(), "channel": k}.get(a.strategy, a.group_size)
+        if a.strategy == "block":
+            g = k
+        v = w.reshape(-1, g)
+        v = (v.abs() / (v.abs().amax(dim=1, keepdim=True) + 1e-6)).reshape(n, k)
+        s = v.sum(0)
+        acc = s if acc is None else acc + s
+        total += n
+    return acc / total
+
+
+def awq_grid_scales_literal(x_mean: torch.Tensor, w_mean: torch.Tensor, ratio: float, duo: bool = True):
+    """One grid point with x_mean / w_mean in bf16: every op of the formula rounds to bf16."""
+    if duo:
+        s = (x_mean.pow(ratio) / (w_mean.pow(1 - ratio) + 1e-4)).clamp(min=1e-4)
+    else:
+        s = x_mean.pow(ratio).clamp(min=1e-4)
+    s = s / (s.max() * s.min()).sqrt()
+    s[torch.isinf(s)] = 1
+    s[torch.isnan(s)] = 1
+    return s
+
+
+def awq_fake_quant_scaled_literal(w: torch.Tensor, s: torch.Tensor, a: QArgs) -> torch.Tensor:
+    """Q(W*s)/s with a bf16 scale vector: W.mul_(s) and the division in bf16."""
+    ws = w * s.view(1, -1)
+    gs = None
+    if a.strategy == "tensor_group":
+        gs = generate_gparam(ws.amin().reshape(1), ws.amax().reshape(1))
+    mn, mx = observe_minmax(ws, a)
+    scale, zp = calculate_qparams(mn, mx, a, global_scale=gs)
+    return fake_quantize(ws, scale, zp, a, global_scale=gs) / s.view(1, -1)

@@ -143,7 +143,8 @@ class CompressionPlan:
     grouped launch (``ops.GroupedQuantize``: the launch ramp paid once per shape, 5 launches for
     all 252 Qwen3-4B linears; one mixed-shape launch per scheme measured 3 % slower, DESIGN §3);
     NVFP4 dense units of one shape are one ``qz_quantize_grouped_nvfp4`` call (two launches);
-    stacked fused experts, FP8_BLOCK and other schemes are one call each.  ``run()`` only enqueues
+    FP8_BLOCK dense units of one shape are one launch of the strip kernel (``qz_quantize_grouped``,
+    qz_block.hip); stacked fused experts and other schemes are one call each.  ``run()`` only enqueues
     the launches (graph/bench friendly, outputs preallocated); ``tensors()`` returns the on-disk tensors by name."""
 
     def __init__(self, units: Sequence[CompressUnit], device, stager=None):
@@ -233,10 +234,12 @@ class CompressionPlan:
                 gq.run(sts[i % len(sts)])
             ops.join_streams(sts)
         if self.singles:
-            nv = [(w, o, a) for u, w, o, a, int_q, fmt in self.singles if a.is_nvfp4 and fmt == ops.default_out_fmt(a)]
+            # float schemes carry fmt None (the kernel's default output, ops._compress_plan)
+            two_stream = lambda a, fmt: a.is_nvfp4 and fmt in (None, ops.default_out_fmt(a))  # noqa: E731
+            nv = [(w, o, a) for u, w, o, a, int_q, fmt in self.singles if two_stream(a, fmt)]
             with torch.cuda.stream(main):
                 for u, w, o, a, int_q, fmt in self.singles:
-                    if not (a.is_nvfp4 and fmt == ops.default_out_fmt(a)):
+                    if not two_stream(a, fmt):
                         ops.quantize_weight(w, a, out_fmt=fmt, out=o)
             # NVFP4 parameters (stacked fused experts): two streams, one's |w| max launch beside
             # the other's encode (ops.quantize_nvfp4_many); grouped by scheme

@@ -35,21 +35,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(ui
 // round an f32 result to bf16 (RNE, v_cvt_pk_bf16_f32) and widen back
 __device__ __forceinline__ float bfr(float f) { return bf2f(f2bf(f)); }
 
-#ifndef QZ_SC1_16
-#define QZ_SC1_16 1  // 16-B output stores write-through (sc1); 0 = plain (tuning knob)
-#endif
 // 16-B write-through (sc1) global store: the line does not stay dirty in the XCD's L2, so the
-// end-of-kernel release has nothing to write back (MI355X_MICROARCH.md: 16-B sc1 store ~ plain).
-// The trailing s_nop keeps the compiler's next instruction off the data VGPRs until the store
-// has read them (cdna_hip_programming.md §5.7).
+// end-of-kernel release has nothing to write back (MI355X_MICROARCH.md: 16-B sc1 store ~ plain;
+// plain 16-B stores measured no faster).  The trailing s_nop keeps the compiler's next
+// instruction off the data VGPRs until the store has read them (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ void st16_wt(void* p, const uint4 v) {
-#if QZ_SC1_16
   typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
   const u32x4_t d = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
-#else
-  *reinterpret_cast<uint4*>(p) = v;
-#endif
 }
 
 // torch.clamp: NaN propagates
@@ -329,5 +322,18 @@ __device__ __forceinline__ GP gp_from_stored(const QP& p, int scale_fmt, const v
   g.fast = (g.s >= 0x1.0p-125f) && (g.s <= 0x1.0p+125f);
   return g;
 }
+
+// ------------------------------------------------ FP8_BLOCK single-pass path (qz_block.hip)
+// n slices of a dense-row batch (tab == nullptr: slice b at w + b * ld_batch, codes / scales
+// batch-major) or n table weights (tab: [4][n] {weight, codes, scales, 0}, qz_quantize_grouped)
+struct BlockFp8Job {
+  const void* w;
+  int64_t n, rows, cols, ld_row, ld_batch;
+  void* q_out;
+  void* s_out;
+  const uint64_t* tab;
+};
+bool block_fp8_ok(const BlockFp8Job& J);
+int block_fp8_launch(const BlockFp8Job& J, const QP& p, hipStream_t st);
 
 }  // namespace qz

@@ -22,26 +22,17 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int BLOCK = 256;
-#ifndef QZ_UNROLL
-#define QZ_UNROLL 2
-#endif
-constexpr int UNROLL = QZ_UNROLL;  // 16-B units per lane per tile
-#ifndef QZ_UNROLL_NT
-#define QZ_UNROLL_NT 2
-#endif
-// units per lane in the nt quantize path (tuning knob): 4 KiB tiles won (72.6 -> 69.3 us at
-// [44032, 4096]) only while the outputs stayed MALL-resident; with distinct outputs per weight
-// UNROLL 2 / 3 / 4 run 17.8 / 19.5 / 20.1 us per weight (grouped launches)
-constexpr int UNROLL_NT = QZ_UNROLL_NT;
+// 16-B units per lane per tile: 2 (round 1: 1 / 3 / 4 slower per weight launch; round 4
+// re-check 23.72 / 24.00 / 20.24 us vs 20.04 us)
+constexpr int UNROLL = 2;
+// units per lane in the nt quantize path: 4 KiB tiles won (72.6 -> 69.3 us at [44032, 4096])
+// only while the outputs stayed MALL-resident; with distinct outputs per weight UNROLL 2 / 3 / 4
+// run 17.8 / 19.5 / 20.1 us per weight (grouped launches)
+constexpr int UNROLL_NT = 2;
 // tile size (units per lane) of a k_group_fast instantiation
 constexpr int tile_unroll(bool fq, bool nt) { return (nt && !fq) ? UNROLL_NT : UNROLL; }
-#ifndef QZ_FAST_BLOCK
-#define QZ_FAST_BLOCK 128
-#endif
-constexpr int FBLOCK = QZ_FAST_BLOCK;  // threads per workgroup of the group path (one tile per wave)
-#ifndef QZ_NUM_CUS
-#define QZ_NUM_CUS 256  // MI355X
-#endif
+// threads per workgroup of the group path (one tile per wave); 64 / 256 measured equal / slower
+constexpr int FBLOCK = 128;
 
 // ------------------------------------------------------------------------ helpers
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
@@ -61,9 +52,7 @@ __device__ __forceinline__ float grp_min(float v) {
   for (int m = 1; m < L; m <<= 1) v = fminf(v, __shfl_xor(v, m, WAVE));
   return v;
 }
-#ifndef QZ_MAX_SEG
-#define QZ_MAX_SEG 8  // shapes per mixed-shape grouped launch
-#endif
+constexpr int QZ_MAX_SEG = 8;  // shapes per mixed-shape grouped launch (qz_quantize_grouped_var)
 struct FastArgs {
   const uint16_t* w;
   int64_t n_units;          // batch*rows*cols/8
@@ -99,56 +88,28 @@ struct FastArgs {
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-#ifndef QZ_HW_FP8
-#define QZ_HW_FP8 1
-#endif
-#ifndef QZ_HW_FP4
-#define QZ_HW_FP4 1
-#endif
-#ifndef QZ_NT_BYTES
-#define QZ_NT_BYTES 268435456  // 256 MiB; fake-quant: weight bytes per launch above which loads are non-temporal
-#endif
+// fake-quant / tile path: weight bytes per launch above which loads are non-temporal (256 MiB)
+constexpr int64_t QZ_NT_BYTES = 268435456;
 // quantize (+pack): weight bytes per launch above which the group path streams non-temporally
 // (nt loads + nt stores).  Measured with DISTINCT output tensors per weight, as a whole-model pass
 // writes them (scripts/tune_fast.py OUTS=48 / MODE=grouped): the read-once weight must not take
 // the MALL from the outputs, at every size -- int4 g128 [11008, 4096] per launch 21.4 -> 20.8 us,
 // FP8 g32 25.3 -> 23.2 us, grouped launches 17.8 -> 17.3 us per weight (the sc1 stores measured
 // better only while one shared output buffer stayed MALL-resident).
-#ifndef QZ_NT_BYTES_Q
-#define QZ_NT_BYTES_Q 0
-#endif
-#ifndef QZ_NT_STORES
-#define QZ_NT_STORES 1  // non-temporal output stores in the NT (large-launch) group path
-#endif
-#ifndef QZ_TILE_NT
-#define QZ_TILE_NT 1  // non-temporal register loads in the tile path above QZ_NT_BYTES
-#endif
-#ifndef QZ_REG_LOADS
-#define QZ_REG_LOADS 0  // per-weight launches: LDS-DMA staging (23.1 -> 21.5 us vs register loads)
-#endif
-#ifndef QZ_REG_LOADS_GRP
-#define QZ_REG_LOADS_GRP 1  // grouped launches: register loads (17.95 -> 17.51 us per weight)
-#endif
-#ifndef QZ_LDS_AUX
-#define QZ_LDS_AUX 0  // cache-policy bits of the LDS-DMA loads (tuning knob)
+constexpr int64_t QZ_NT_BYTES_Q = 0;  // i.e. every quantize launch; its nt path stores non-temporally too
+// per-weight launches stage through LDS-DMA (23.1 -> 21.5 us vs register loads), grouped launches
+// load to registers (17.95 -> 17.51 us per weight): k_group_fast's REG = GRP
+#ifndef QZ_BLK_FAST
+#define QZ_BLK_FAST 1  // FP8_BLOCK 128x128 through qz_block.hip's strip kernel (0: the round-1 k_tile_fast)
 #endif
 
-// round both lanes of an f32 pair to bf16 and widen back.  QZ_BFR_ZERO_HI: one
-// v_cvt_pk_bf16_f32(0, v) per lane puts bf16(v) in the HIGH half over a zero low half -- the f32
-// value bf16(v) itself -- so 2 VALU per pair instead of a packed convert + 2 unpacks (3)
-#ifndef QZ_BFR_ZERO_HI
-#define QZ_BFR_ZERO_HI 1
-#endif
+// round both lanes of an f32 pair to bf16 and widen back: one v_cvt_pk_bf16_f32(0, v) per lane
+// puts bf16(v) in the HIGH half over a zero low half -- the f32 value bf16(v) itself -- so 2 VALU
+// per pair instead of a packed convert + 2 unpacks (3)
 __device__ __forceinline__ f32x2 bfr2(f32x2 v) {
   f32x2 r;
-#if QZ_BFR_ZERO_HI
   r.x = __uint_as_float(__builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){0.0f, v.x}, bf16x2)));
   r.y = __uint_as_float(__builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){0.0f, v.y}, bf16x2)));
-#else
-  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
-  r.x = __uint_as_float(u << 16);
-  r.y = __uint_as_float(u & 0xffff0000u);
-#endif
   return r;
 }
 
@@ -169,9 +130,6 @@ __device__ __forceinline__ float bf16_div(float d, float c) {
 // 33.7 -> 31.1 us, FP8_BLOCK 25.4 -> 23.6 us; scripts/tune_ab.sh).  In the nt quantize path nt
 // stores win once the outputs are distinct per weight (QZ_NT_BYTES_Q).  The 2-byte scale stores
 // stay plain: as sc1 each is its own fabric write (no gain measured).
-#ifndef QZ_SC1
-#define QZ_SC1 2  // 0 = plain stores, 1 = sc1 code + scale stores, 2 = sc1 code stores
-#endif
 // sc1 store (relaxed agent-scope atomic store = global_store_* sc1)
 template <typename T>
 __device__ __forceinline__ void st_sc1(T* p, const T v) {
@@ -192,9 +150,9 @@ __device__ __forceinline__ void st_sc1(T* p, const T v) {
 // output stores; NTS = non-temporal (streaming outputs of launches far larger than the MALL)
 template <bool NTS, typename T>
 __device__ __forceinline__ void st_out(T* p, const T v) {
-  if constexpr (QZ_SC1 != 0 && !NTS && sizeof(T) <= 8) {
+  if constexpr (!NTS && sizeof(T) <= 8) {
     st_sc1(p, v);
-  } else if constexpr (QZ_SC1 != 0 && !NTS && sizeof(T) == 16) {
+  } else if constexpr (!NTS && sizeof(T) == 16) {
     st16_wt(p, __builtin_bit_cast(uint4, v));
   } else if constexpr (NTS) {
     if constexpr (sizeof(T) == 4) {
@@ -245,7 +203,7 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
   // only their top 2 mantissa bits set, so q can round differently from x / s only if its low
   // 21 mantissa bits are within 4 of zero (mod 2^21); such pairs (and +-0, which needs the
   // signed-zero rule) take the IEEE division.  Exact grid values may be flagged too (harmless).
-  if (KIND == K_NV && !FQ && QZ_HW_FP4) {
+  if (KIND == K_NV && !FQ) {
     // near: the low 21 bits of (bits + 4) below 8, i.e. ((bits << 11) + (4 << 11)) < (8 << 11)
     // (one v_lshl_add_u32 each), either element of the pair (v_min_u32); each pair's two codes
     // go straight into byte k of the word (the conversion's destination-byte select)
@@ -344,16 +302,12 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (KIND == K_FP8) {
-#if QZ_HW_FP8  // v_cvt_pk_fp8_f32 (OCP e4m3, RNE); exhaustively checked vs torch's cast
+        // v_cvt_pk_fp8_f32 (OCP e4m3, RNE); exhaustively checked vs torch's cast
         const uint32_t pk = (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f),
                                                                       __builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f), 0, false);
         c[2 * k] = pk & 0xffu;
         c[2 * k + 1] = (pk >> 8) & 0xffu;
-#else
-        c[2 * k] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].x, -448.f, 448.f)));
-        c[2 * k + 1] = bf16_to_e4m3(f2bf(__builtin_amdgcn_fmed3f(t[k].y, -448.f, 448.f)));
-#endif
-      } else if (QZ_HW_FP4) {
+      } else {
         // v_cvt_scalef32_pk_fp4_f32: RNE on the E2M1 grid == cast_to_fp4's thresholds (checked
         // exhaustively); "+ 0" maps an exact -0 input to +0 (torch.sign(-0.) is 0 -> code 0),
         // small negatives still round to -0 (code 8) as sign(x)*|q| does
@@ -362,9 +316,6 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
         const uint32_t pk = __builtin_amdgcn_cvt_scalef32_pk_fp4_f32(0u, ca, cb, 1.0f, 0);
         c[2 * k] = pk & 0xfu;
         c[2 * k + 1] = (pk >> 4) & 0xfu;
-      } else {
-        c[2 * k] = fp4_code(__builtin_amdgcn_fmed3f(t[k].x, -6.f, 6.f));
-        c[2 * k + 1] = fp4_code(__builtin_amdgcn_fmed3f(t[k].y, -6.f, 6.f));
       }
     }
     if (FQ) {
@@ -449,8 +400,7 @@ __device__ __forceinline__ void process_unit(const FastArgs& A, const QP& p, con
   if ((lane & (L - 1)) == 0) {
     const int64_t gi = unit >> LOGL;
     if (A.scale_bytes == 2) {
-      if constexpr (QZ_SC1 == 1 && !NTS) st_sc1(reinterpret_cast<uint16_t*>(A.s_out) + gi, (uint16_t)g.sbits);
-      else reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
+      reinterpret_cast<uint16_t*>(A.s_out)[gi] = (uint16_t)g.sbits;
     } else {
       reinterpret_cast<uint8_t*>(A.s_out)[gi] = (uint8_t)g.sbits;
     }
@@ -518,7 +468,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
   }
   const uint4* src = reinterpret_cast<const uint4*>(A.w + b * A.ld_batch);
   // direct-to-register 16-B loads (grouped launches) or LDS-DMA staging (per-weight launches)
-  constexpr bool REG = GRP ? QZ_REG_LOADS_GRP : QZ_REG_LOADS;
+  constexpr bool REG = GRP;
   uint4 v[UNROLL];
   if constexpr (REG) {
 #pragma unroll
@@ -535,7 +485,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
       unit = unit < A.units_per_batch ? unit : A.units_per_batch - 1;
       __builtin_amdgcn_global_load_lds((const void*)(src + unit),
                                        (__attribute__((address_space(3))) void*)&lds_buf[w][u][0], 16, 0,
-                                       NT ? 2 : QZ_LDS_AUX);
+                                       NT ? 2 : 0);
     }
   }
   // AWQ fake-quant: fetch this lane's column scales while the DMA is in flight
@@ -561,7 +511,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) v[u] = lds_buf[w][u][lane];
   }
-  process_tile<LOGL, KIND, FQ, SYM, NT && QZ_NT_STORES, UNROLL>(A, p, v, b, tile, lane, csu);
+  process_tile<LOGL, KIND, FQ, SYM, NT, UNROLL>(A, p, v, b, tile, lane, csu);
 }
 
 // ------------------------------------------------ AWQ fake-quant with column scales
@@ -573,10 +523,7 @@ __global__ __launch_bounds__(FBLOCK) void k_group_fast(FastArgs A0) {
 // VALU-bound (PMC r02c: 41.9 us for [11008, 4096], 0.54 of 8 TB/s).  grid = (column chunks of
 // 64 units, row blocks / waves per workgroup, batch): consecutive workgroups cover one row
 // block's chunks, so the stream stays contiguous.
-#ifndef QZ_FQ_ROWS
-#define QZ_FQ_ROWS 4
-#endif
-constexpr int FQ_ROWS = QZ_FQ_ROWS;
+constexpr int FQ_ROWS = 4;  // rows per tile: 2 / 4 / 8 = 31.93 / 30.37 / 33.25 us (r02e)
 
 // bf16(d / c) for a pair given r = rcp(c), packed: the IEEE division only when a quotient lies
 // within 4 ulps of a bf16 rounding midpoint (low 16 bits near 0x8000; 16-bit adds) or when
@@ -710,15 +657,9 @@ __device__ __forceinline__ void fq_load_tile(uint4 (&v)[U], const uint4* src, in
   }
 }
 
-#ifndef QZ_FQ_ST_AUX
-#define QZ_FQ_ST_AUX 16  // cache policy of the buffer stores: sc1 (gfx950 CPol SC1 = 16)
-#endif
-#ifndef QZ_FQ_LD_AUX
-#define QZ_FQ_LD_AUX 0  // cache policy of the one-tile fake-quant's weight loads (A/B knob; 2 = nt)
-#endif
-#ifndef QZ_FQ_BUF
-#define QZ_FQ_BUF 1  // 1: one-tile waves load / store through wave-uniform buffer descriptors (A/B knob)
-#endif
+// buffer stores sc1 (gfx950 CPol SC1 = 16), weight loads default policy: nt loads / stores and
+// plain stores measured equal or slower in the AWQ grid's pattern (r04v / r04ad)
+constexpr int FQ_ST_AUX = 16, FQ_LD_AUX = 0;
 // wave-uniform 64-bit value, provably so to the compiler (SGPRs)
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) |
@@ -742,7 +683,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
   // one tile per wave: the tile's rows through one source and one destination descriptor
   // (wave-uniform bases, 32-bit lane / row offsets: no per-unit 64-bit address arithmetic); rows
   // past the slice re-read its last row and are not stored, nor are lanes past the last column
-  constexpr bool BUF = QZ_FQ_BUF && !NT;
+  constexpr bool BUF = !NT;  // wave-uniform buffer descriptors (the nt variant uses global loads)
   uint32_t voff = 0, roff[U];
   __amdgpu_buffer_rsrc_t rs_dst;
   int nrow_b = 0;
@@ -760,7 +701,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
         0x00020000);
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], QZ_FQ_LD_AUX));
+      v[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs_src, voff, roff[u], FQ_LD_AUX));
   } else {
     fq_load_tile<NT, U>(v, src, rblk * U, rows, upr, cuc);
   }
@@ -783,7 +724,7 @@ __global__ __launch_bounds__(FBLOCK) void k_fq_cols(FastArgs A, int64_t rows) {
     for (int u = 0; u < U; ++u) {
       const uint4 o = fq_unit<LOGL, KIND, SYM>(p, v[u], cs, rc, cs_ok);
       if (col_ok && u < nrow_b)  // sc1 (write-through) as st_out
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs_dst, voff, roff[u], QZ_FQ_ST_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs_dst, voff, roff[u], FQ_ST_AUX);
     }
     return;
   }
@@ -1554,7 +1495,11 @@ int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st
   if (rc) return rc;
   if (tab) hipLaunchKernelGGL(k_nv_encode<true>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
   else hipLaunchKernelGGL(k_nv_encode<false>, dim3((unsigned)grid), dim3(NV_BLOCK), 0, st, A);
-  return launch_err();
+  rc = launch_err();
+  // the |w| max launch has run but the encode (which resets the sync lines) has not: clear them,
+  // so the region is zero for the next call on this stream as the contract says
+  if (rc) hipMemsetAsync(A.sync, 0, 4 * NV_SYNC_STRIDE * (size_t)A.n_slices, st);
+  return rc;
 }
 
 }  // namespace
@@ -1581,13 +1526,9 @@ const char* qz_strerror(int code) {
 int qz_version(void) { return 200; }
 
 const char* qz_build_config(void) {
-#define QZ_STR2(x) #x
-#define QZ_STR(x) QZ_STR2(x)
-  return "nt_bytes_q=" QZ_STR(QZ_NT_BYTES_Q) ";nt_bytes_fq=" QZ_STR(QZ_NT_BYTES) ";unroll=" QZ_STR(QZ_UNROLL)
-         ";unroll_nt=" QZ_STR(QZ_UNROLL_NT) ";fast_block=" QZ_STR(QZ_FAST_BLOCK) ";reg_loads=" QZ_STR(QZ_REG_LOADS)
-         ";reg_loads_grp=" QZ_STR(QZ_REG_LOADS_GRP) ";arch=gfx950";
-#undef QZ_STR
-#undef QZ_STR2
+  // the constants above (k_group_fast's NT instantiation = weight bytes > nt_bytes_q)
+  return "nt_bytes_q=0;nt_bytes_fq=268435456;unroll=2;unroll_nt=2;fast_block=128;reg_loads=0;reg_loads_grp=1;"
+         "arch=gfx950";
 }
 
 size_t qz_quantize_workspace_size(int64_t batch, int64_t rows, int64_t cols, const qz_args* a) {
@@ -1673,11 +1614,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const bool nt = batch * rows * cols * 2 > (fq ? QZ_NT_BYTES : QZ_NT_BYTES_Q);
-#ifndef QZ_FQ_COLS
-#define QZ_FQ_COLS 1  // column-tiled AWQ fake-quant kernel (0: unit-wise k_group_fast, A/B knob)
-#endif
     const int64_t fq_yblocks = cdiv(cdiv(rows, FQ_ROWS), FBLOCK / WAVE);
-    FqcFn fqc = (QZ_FQ_COLS && fq && col_scales) ? pick_fqc(logl, pl.kind, pl.p.sym != 0, nt) : nullptr;
+    FqcFn fqc = (fq && col_scales) ? pick_fqc(logl, pl.kind, pl.p.sym != 0, nt) : nullptr;
     if (fqc && fq_yblocks <= 65535) {
       hipLaunchKernelGGL(fqc, dim3((unsigned)cdiv(F.units_per_row, WAVE), (unsigned)fq_yblocks, (unsigned)batch),
                          dim3(FBLOCK), 0, st, F, rows);
@@ -1688,6 +1626,13 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
                        dim3(FBLOCK), 0, st, F);
     return launch_err();
+  }
+
+  // FP8_BLOCK 128 x 128 (qz_block.hip): strips of NB blocks per workgroup, 16-B code stores
+  if (QZ_BLK_FAST && a->strategy == QZ_BLOCK && pl.kind == K_FP8 && out_fmt == QZ_OUT_FP8 && a->block_h == 128 &&
+      a->block_w == 128) {
+    BlockFp8Job J{w, batch, rows, cols, ld_row, batch > 1 ? ld_batch : rows * ld_row, q_out, s_dst, nullptr};
+    if (block_fp8_ok(J)) return block_fp8_launch(J, pl.p, st);
   }
 
   // single-pass tile path: BLOCK tiles, CHANNEL rows, wide groups (one workgroup per group)
@@ -1728,7 +1673,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       const int64_t tiles = (rows / th) * (cols / tw);
       int maxu = 1;
       while (maxu * BLOCK < U) maxu *= 2;
-      const bool nt = QZ_TILE_NT && batch * rows * cols * 2 > QZ_NT_BYTES;
+      const bool nt = batch * rows * cols * 2 > QZ_NT_BYTES;
       hipLaunchKernelGGL(pick_tile(pl.kind, pl.p.sym != 0, maxu, nt), dim3((unsigned)tiles, (unsigned)batch), dim3(BLOCK),
                          0, st, F, T);
       return launch_err();
@@ -1782,6 +1727,12 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
   int rc = make_plan(a, rows, cols, &pl);
   if (rc) return rc;
   if ((rc = check_out_fmt(pl, out_fmt))) return rc;
+  if (a->strategy == QZ_BLOCK) {  // FP8_BLOCK 128 x 128: one strip-kernel launch over the table
+    if (!QZ_BLK_FAST || pl.kind != K_FP8 || out_fmt != QZ_OUT_FP8 || a->block_h != 128 || a->block_w != 128)
+      return QZ_ERR_FORMAT;
+    BlockFp8Job J{nullptr, n, rows, cols, cols, rows * cols, nullptr, nullptr, table};
+    return block_fp8_ok(J) ? block_fp8_launch(J, pl.p, (hipStream_t)stream) : QZ_ERR_FORMAT;
+  }
   const int64_t g = a->group_size;
   const bool grp = a->strategy == QZ_GROUP || a->strategy == QZ_TENSOR_GROUP;
   const bool pow2 = g >= 8 && g <= 512 && (g & (g - 1)) == 0;

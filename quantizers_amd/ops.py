@@ -92,6 +92,14 @@ def sync_workspace(n_slices: int, device, stream=None) -> torch.Tensor:
     return buf
 
 
+def _drop_sync(device, stream=None) -> None:
+    """Forget the stream's NVFP4 sync region after a failed call (the library clears it on the
+    stream too; a fresh zeroed region is allocated by the next call either way)."""
+    dev = torch.device(device)
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
+    _sync_cache.pop((dev.index or 0, st.cuda_stream), None)
+
+
 def _nvfp4_fused_ok(a: QuantizationArgs, out_fmt: int, geom, w: torch.Tensor) -> bool:
     b, r, c, ld_r, ld_b = geom
     return (a.is_nvfp4 and a.group_size == 16 and out_fmt == _lib.QZ_OUT_FP4_PACKED and ld_r == c
@@ -201,6 +209,8 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
         sync = sync_workspace(b, dev)
         rc = lib.qz_quantize_nvfp4(_ptr(w), b, r, c, ld_b, ctypes.byref(ca), _ptr(o["codes"]), _ptr(o["scale"]),
                                    _ptr(o["global_scale"]), _ptr(sync), sync.numel(), _stream())
+        if rc:
+            _drop_sync(dev)
         _lib.check(rc, "qz_quantize_nvfp4")
         o.pop("workspace", None)
         return o
@@ -216,15 +226,24 @@ def quantize_weight(w: torch.Tensor, a: QuantizationArgs, out_fmt: Optional[int]
     return o
 
 
+def is_fp8_block128(a: QuantizationArgs) -> bool:
+    """compressed-tensors' FP8_BLOCK preset: e4m3 codes, one bf16 scale per 128 x 128 block."""
+    return (a.strategy == "block" and a.type == "float" and a.num_bits == 8
+            and list(a.block_structure or ()) == [128, 128])
+
+
 def grouped_ok(a: QuantizationArgs, w: torch.Tensor) -> bool:
     """True when one grouped launch covers this scheme and weight: qz_quantize_grouped (the
-    single-pass group path) or, for NVFP4, qz_quantize_grouped_nvfp4 (two launches per group)."""
+    single-pass group path, or FP8_BLOCK's strip kernel) or, for NVFP4,
+    qz_quantize_grouped_nvfp4 (two launches per group)."""
+    dense = w.dim() == 2 and w.is_contiguous() and w.dtype == torch.bfloat16 and w.data_ptr() % 16 == 0
+    if is_fp8_block128(a):
+        return dense and w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
     g = a.group_size or 0
     if a.is_nvfp4 and g != 16:
         return False
     return (a.strategy in ("group", "tensor_group") and 8 <= g <= 512 and (g & (g - 1)) == 0
-            and w.dim() == 2 and w.is_contiguous() and w.dtype == torch.bfloat16 and w.shape[1] % g == 0
-            and w.data_ptr() % 16 == 0)
+            and dense and w.shape[1] % g == 0)
 
 
 def _check_no_alias(ws: Sequence[torch.Tensor], outs: Sequence[Dict[str, torch.Tensor]]) -> None:
@@ -284,11 +303,15 @@ class GroupedQuantize:
         shapes = [tuple(w.shape) for w in ws]
         self.mixed = len(set(shapes)) > 1
         self.nvfp4 = a.is_nvfp4
-        if self.nvfp4 and self.mixed:
-            raise ValueError("GroupedQuantize: NVFP4 weights of one launch must share one shape")
+        if (self.nvfp4 or is_fp8_block128(a)) and self.mixed:
+            raise ValueError("GroupedQuantize: NVFP4 / FP8_BLOCK weights of one launch must share one shape")
         self.a = a
         dev = ws[0].device
         self.out_fmt = default_out_fmt(a) if out_fmt is None else out_fmt
+        if self.nvfp4 and self.out_fmt != _lib.QZ_OUT_FP4_PACKED:
+            # qz_quantize_grouped_nvfp4 writes packed E2M1 codes only
+            raise ValueError("GroupedQuantize: NVFP4 grouped launches write packed FP4 codes only "
+                             "(use quantize_weight for other output formats)")
         self.ca = a.to_c()
         if outs is None:
             outs = [alloc_outputs(shp, a, self.out_fmt, dev) for shp in shapes]
@@ -325,6 +348,8 @@ class GroupedQuantize:
             sync = sync_workspace(self.n, self.weights[0].device, stream)
             rc = self.lib.qz_quantize_grouped_nvfp4(self.n, _ptr(self.table), self.rows, self.cols, ctypes.byref(self.ca),
                                                     _ptr(sync), sync.numel(), st)
+            if rc:
+                _drop_sync(self.weights[0].device, stream)
             _lib.check(rc, "qz_quantize_grouped_nvfp4")
             return self.outs
         if self.mixed:
@@ -346,8 +371,9 @@ def quantize_weights(ws: Sequence[torch.Tensor], a: QuantizationArgs,
     ``quantize_weight`` launch per weight.  Results are identical either way."""
     res: List[Optional[Dict[str, torch.Tensor]]] = [None] * len(ws)
     by_shape: Dict[tuple, List[int]] = {}
+    nv_other_fmt = a.is_nvfp4 and out_fmt not in (None, _lib.QZ_OUT_FP4_PACKED)
     for i, w in enumerate(ws):
-        if grouped_ok(a, w):
+        if grouped_ok(a, w) and not nv_other_fmt:
             by_shape.setdefault((tuple(w.shape), w.device), []).append(i)
         else:
             res[i] = quantize_weight(w, a, out_fmt)

@@ -67,9 +67,9 @@ def _per_batch_mm(a, b):
                     "as per-batch 2-D GEMMs", key[0], key[1], PINNED_BMM_K)
     lead = a.shape[:-2]
     a3, b3 = a.reshape(-1, *a.shape[-2:]), b.reshape(-1, *b.shape[-2:])
-    out = torch.empty(a3.shape[0], a.shape[-2], b.shape[-1], dtype=a.dtype, device=a.device)
-    for i in range(a3.shape[0]):
-        torch.mm(a3[i], b3[i], out=out[i])
+    # torch.stack of plain mm results (no out=): stays autograd-safe if a forward inside the
+    # guard runs with grad enabled
+    out = torch.stack([torch.mm(a3[i], b3[i]) for i in range(a3.shape[0])])
     return out.reshape(*lead, a.shape[-2], b.shape[-1])
 
 
@@ -87,6 +87,8 @@ def bmm_guard():
     saved = (torch.bmm, torch.matmul, torch.Tensor.matmul, torch.Tensor.__matmul__)
 
     def wrap(orig):
+        # anything but the defect's operands goes to the original, whose result is returned as is:
+        # Tensor.__matmul__'s NotImplemented for a non-tensor operand (so __rmatmul__ runs) included
         def f(a, b, *args, **kw):
             if not args and not kw and pinned_bmm_defect(a, b):
                 return _per_batch_mm(a, b)

@@ -189,10 +189,16 @@ class Residency:
         """Non-layer tensors on every rank's device (rank 0 moves its own there first)."""
         ss = slots(model, exclude=layers)
         if self.rank == 0:
+            # id(host tensor) -> (that tensor, kept alive so its id stays unique; its device copy)
+            moved: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
             for s in ss:
                 t = _get(s)
-                if t.device != self.device:
+                if id(t) in moved:  # a tied slot (lm_head under tie_word_embeddings): the SAME new object
+                    m, is_buf, name = s
+                    (m._buffers if is_buf else m._parameters)[name] = moved[id(t)][1]
+                elif t.device != self.device:
                     _set(s, t.detach().to(self.device))
+                    moved[id(t)] = (t, _get(s))
         broadcast_slots(ss, self.device)
 
     def release_outside(self, model: nn.Module, layers: nn.ModuleList) -> None:

@@ -109,3 +109,22 @@ def test_skeleton_rank_save_byte_identical(cuda, tmp_path):
     assert files == sorted(os.listdir(multi)) and len([f for f in files if f.endswith(".safetensors")]) >= 2
     for fn in files:
         assert filecmp.cmp(os.path.join(one, fn), os.path.join(multi, fn), shallow=False), fn
+
+
+def test_materialise_outside_keeps_ties(cuda):
+    """rank 0's host-resident non-layer tensors moved to the device keep their ties --
+    tie_word_embeddings' lm_head.weight stays the very Parameter embed_tokens holds, so the
+    broadcast sends it once and the checkpoint gets no untied copy."""
+    from transformers import AutoModelForCausalLM, Qwen3Config
+    from quantizers_amd import residency
+    cfg = Qwen3Config(hidden_size=128, intermediate_size=256, num_hidden_layers=1, num_attention_heads=2,
+                      num_key_value_heads=1, head_dim=64, vocab_size=256, tie_word_embeddings=True)
+    m = AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)  # host-resident, as rank 0's RTN model
+    assert m.lm_head.weight is m.model.embed_tokens.weight
+    res = residency.Residency(m, cuda, 1 << 30)
+    res.materialise_outside(m, m.model.layers)
+    assert m.model.embed_tokens.weight.is_cuda
+    assert m.lm_head.weight is m.model.embed_tokens.weight
+    ss = residency.slots(m, exclude=m.model.layers)
+    alias = residency._alias_groups(ss)
+    assert sum(1 for i, a in enumerate(alias) if a != i) == 1  # one tied slot, sent once

@@ -643,18 +643,67 @@ def test_quantize_many_equals_single_calls(cuda):
     assert torch.equal(outs[0]["codes"].cpu(), ref[-1]["weight_packed"].cpu())
 
 
-@pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "int8_g64_sym", "fp8_g32", "mxfp4_g32"])
+FP8_BLOCK = dict(num_bits=8, type="float", strategy="block", block_structure=[128, 128])
+
+
+@pytest.mark.parametrize("shape", [(128, 128), (256, 256), (384, 384), (128, 640), (256, 768), (512, 2560),
+                                   (1024, 4096)])
+def test_fp8_block_strip_widths_c_oracle(cuda, shape):
+    """FP8_BLOCK's strip kernel (qz_block.hip) at every strip width it picks -- 1, 2 or 4 blocks per
+    workgroup from cols / 128 = 1, 2, 3, 5, 6, 20, 32 -- and on a row-strided view (the same
+    weight's columns inside a wider tensor, ld_row > cols): codes and block scales bit-identical to
+    the plain-C oracle (edge weight: outliers, an all-zero block row start, exact ties)."""
+    import qref
+    a = QuantizationArgs(**FP8_BLOCK)
+    r, c = shape
+    w = _edge_weight(r, c, 128, seed=r + c)
+    want = qref.compress_weight(w, _oracle_args(a))
+    got = ops.compress_weight(w.to(cuda), a)
+    _eq(got["weight"], want["weight"])
+    _eq(got["weight_scale"], want["weight_scale"])
+    wide = torch.zeros(r, c + 256, dtype=torch.bfloat16, device=cuda)
+    wide[:, 64:64 + c] = w.to(cuda)
+    q = ops.quantize_weight(wide[:, 64:64 + c], a)  # ld_row = c + 256, 128-B aligned start
+    _eq(q["codes"], want["weight"])
+    _eq(q["scale"], want["weight_scale"])
+
+
+def test_fp8_block_batch_and_zero_blocks(cuda):
+    """A strided [E, r, c] batch (every other slice of a stack) through the strip kernel == per
+    slice; an all-zero block gets the eps scale (D1) and zero codes, a block holding +-448 * s ties
+    rounds as the oracle does."""
+    import qref
+    a = QuantizationArgs(**FP8_BLOCK)
+    g = torch.Generator(device=cuda).manual_seed(12)
+    stack = (torch.randn(6, 256, 512, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    stack[2, :128, :128] = 0
+    stack[4, 128:, 384:] *= 1000
+    view = stack[::2]  # ld_batch = 2 * 256 * 512
+    got = ops.quantize_weight(view, a)
+    for i in range(3):
+        want = qref.compress_weight(view[i].cpu(), _oracle_args(a))
+        _eq(got["codes"][i], want["weight"])
+        _eq(got["scale"][i], want["weight_scale"])
+    assert got["scale"][1, 0, 0].float().item() == 0.0078125 and not got["codes"][1, :128, :128].view(torch.uint8).any()
+
+
+@pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "int8_g64_sym", "fp8_g32", "mxfp4_g32",
+                                    "fp8_block128"])
 def test_quantize_grouped_equals_single_calls(cuda, scheme):
     """qz_quantize_grouped (n weights, ONE launch, per-weight pointer table) == quantize_weight per
     weight, bit for bit, in the small-launch path (3 weights) and in the large-launch path
-    (nt loads, UNROLL 4 tiles: 9 x [4096, 4096] = 302 MB > 256 MiB)."""
+    (nt loads, UNROLL 4 tiles: 9 x [4096, 4096] = 302 MB > 256 MiB).  FP8_BLOCK: the strip kernel
+    in table mode (shapes divisible by its 128 x 128 blocks)."""
     a = {"int4_g128_sym": QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128),
          "int4_g32_asym": QuantizationArgs(num_bits=4, type="int", symmetric=False, group_size=32),
          "int8_g64_sym": QuantizationArgs(num_bits=8, type="int", symmetric=True, group_size=64),
          "fp8_g32": QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32),
-         "mxfp4_g32": QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")}[scheme]
-    for n, (r, c) in ((3, (96, 1024)), (9, (4096, 4096))):
-        ws = [_edge_weight(r, c, a.group_size, seed=s).to(cuda) for s in range(n)]
+         "mxfp4_g32": QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8"),
+         "fp8_block128": QuantizationArgs(**FP8_BLOCK)}[scheme]
+    block = scheme == "fp8_block128"
+    gsz = 128 if block else a.group_size
+    for n, (r, c) in ((3, (128, 1024) if block else (96, 1024)), (9, (4096, 4096))):
+        ws = [_edge_weight(r, c, gsz, seed=s).to(cuda) for s in range(n)]
         ref = [ops.quantize_weight(w, a) for w in ws]
         got = ops.GroupedQuantize(ws, a).run()
         torch.cuda.synchronize()
@@ -665,8 +714,9 @@ def test_quantize_grouped_equals_single_calls(cuda, scheme):
                 assert torch.equal(o["zero_point"].cpu(), rf["zero_point"].cpu())
         del ws, ref, got
     # quantize_weights: grouped per shape + per-weight launches for the rest, same results
-    mix = [_edge_weight(64, 256, a.group_size, seed=7).to(cuda), _edge_weight(32, 512, a.group_size, seed=8).to(cuda),
-           _edge_weight(64, 256, a.group_size, seed=9).to(cuda)]
+    shp = ((128, 256), (256, 512)) if block else ((64, 256), (32, 512))
+    mix = [_edge_weight(*shp[0], gsz, seed=7).to(cuda), _edge_weight(*shp[1], gsz, seed=8).to(cuda),
+           _edge_weight(*shp[0], gsz, seed=9).to(cuda)]
     for o, w in zip(ops.quantize_weights(mix, a), mix):
         rf = ops.quantize_weight(w, a)
         assert torch.equal(o["codes"].cpu(), rf["codes"].cpu())
@@ -790,6 +840,44 @@ def test_whole_model_plan_equals_per_weight(cuda):
     torch.cuda.empty_cache()
 
 
+def test_whole_model_plan_mixed_fp8_block_int4(cuda):
+    """BASELINE.json configs[2] through the product: the mixed recipe (FP8_BLOCK q/k/v/o + int4 g32
+    gate/up/down, configs/recipes/mixed_fp8_block_awq_int4.yaml = the reference's
+    recipe_mixed_fp8_int4.yaml, quirk M1 corrected) on the Qwen3-4B model is 5 grouped launches --
+    q, k+v and o through the FP8_BLOCK strip kernel, gate+up and down through the group kernel --
+    and every on-disk tensor equals the per-weight launch; one weight per shape also vs the
+    plain-C oracle."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import qref
+    from quantizers_amd.compressor import CompressionPlan, compression_units
+    torch.manual_seed(6)
+    model = bench.build_model(cuda, bench.MIXED_RECIPE)
+    units, _ = compression_units(model)
+    plan = CompressionPlan(units, cuda)
+    assert len(units) == 252 and plan.launches == 5 and not plan.singles
+    assert sum(1 for gq, *_ in plan.grouped if ops.is_fp8_block128(gq.a)) == 3
+    plan.run()
+    got = plan.tensors()
+    seen = set()
+    for u in units:
+        w = u.refs[0].weight
+        ref = ops.compress_weight(w, u.scheme.weights)
+        for k, v in ref.items():
+            _eq(got[f"{u.refs[0].name}.{k}"], v)
+        if tuple(w.shape) not in seen:
+            seen.add(tuple(w.shape))
+            want = qref.compress_weight(w.cpu(), _oracle_args(u.scheme.weights))
+            for k, v in want.items():
+                if not k.startswith("_"):
+                    _eq(got[f"{u.refs[0].name}.{k}"], v)
+    assert len(seen) == 5
+    del model, plan, got
+    torch.cuda.empty_cache()
+
+
 def test_whole_model_plan_nvfp4_two_streams(cuda):
     """recipe_Dense_NVFP4 on the Qwen3-4B model: the CompressionPlan's 7 grouped NVFP4 calls, run
     over two streams (ops.nvfp4_streams), give every on-disk tensor bit-identical to the per-weight
@@ -862,3 +950,66 @@ def test_stats_one_launch_stress_many_grids(cuda):
             assert torch.equal(out.cpu(), want), (case, which, rows, cols, g, rep)
     for buf in ops._stats_ws_cache.values():
         assert not buf[:32768].any()
+
+
+def _slices_vs_single_and_oracle(stack_view, a, out, oracle_slices):
+    """Every slice of a batched launch's outputs == the per-slice launch; ``oracle_slices`` of them
+    also == the plain-C oracle."""
+    import qref
+    for e in range(stack_view.shape[0]):
+        one = ops.quantize_weight(stack_view[e], a)
+        _eq(out["codes"][e], one["codes"])
+        _eq(out["scale"][e], one["scale"])
+    for e in oracle_slices:
+        want = qref.compress_weight(stack_view[e].cpu(), _oracle_args(a))
+        codes = want.get("weight_packed", want.get("weight"))
+        _eq(out["codes"][e], codes)
+        _eq(out["scale"][e], want["weight_scale"])
+
+
+def test_bench_config4_mxfp4_expert_halves_full_size(cuda):
+    """VERDICT r04 item 3, BASELINE.json configs[3] exactly as bench.py times it: MXFP4 over the
+    strided gate / up halves gu[:, :768], gu[:, 768:] of one Qwen3-30B-A3B fused parameter
+    [128, 1536, 2048] and over the down projections [128, 2048, 768] -- one launch each through the
+    non-temporal path (403 MB / 201 MB per launch) -- every slice equals its own launch, two slices
+    per launch equal the plain-C oracle (reference configs/test-quantize_qwen3_30b_a3b_nvfp4.yaml:18-25
+    names the model; MXFP4 is BASELINE's scheme)."""
+    mx = QuantizationArgs(num_bits=4, type="float", group_size=32, scale_dtype="uint8")
+    g = torch.Generator(device=cuda).manual_seed(31)
+    gu = (torch.randn(128, 1536, 2048, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    gu[7, 100, :64] *= 300  # outliers in one slice
+    dn = (torch.randn(128, 2048, 768, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    for view in (gu[:, :768], gu[:, 768:], dn):
+        assert view.numel() * 2 > 200 << 20
+        out = ops.quantize_weight(view, mx)
+        _slices_vs_single_and_oracle(view, mx, out, (7, 127))
+        del out
+
+
+def test_bench_config5_minimax_full_size(cuda):
+    """VERDICT r04 item 3, BASELINE.json configs[4] as bench.py's minimax_pass times it
+    (recipe_Minimax-M2.1-AWQ-MixedPrec.yaml:24-48): int4 sym g32 over the strided w1 / w3 halves of
+    a fused [256, 3072, 3072] parameter and the w2 [256, 3072, 1536] stack, FP8 g32 over the
+    attention q [6144, 3072] and o [3072, 6144]: every slice == its own launch, two slices per
+    launch and both attention weights == the plain-C oracle."""
+    import qref
+    i4 = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    f8 = QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32)
+    g = torch.Generator(device=cuda).manual_seed(32)
+    gu = (torch.randn(256, 3072, 3072, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    for view in (gu[:, :1536], gu[:, 1536:]):
+        out = ops.quantize_weight(view, i4)
+        _slices_vs_single_and_oracle(view, i4, out, (0, 255))
+        del out
+    del gu
+    dn = (torch.randn(256, 3072, 1536, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    out = ops.quantize_weight(dn, i4)
+    _slices_vs_single_and_oracle(dn, i4, out, (3, 200))
+    del dn, out
+    for r, c in ((6144, 3072), (3072, 6144)):
+        w = (torch.randn(r, c, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+        got = ops.compress_weight(w, f8)
+        want = qref.compress_weight(w.cpu(), _oracle_args(f8))
+        _eq(got["weight"], want["weight"])
+        _eq(got["weight_scale"], want["weight_scale"])
+    torch.cuda.empty_cache()

@@ -65,3 +65,22 @@ def test_bmm_guard_routes_only_the_pinned_fault_class(monkeypatch):
     with patching.bmm_guard():  # the real routing: per-batch torch.mm, same values as a float product
         got = torch.bmm(x, nt)
     assert torch.allclose(got.float(), want.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_bmm_guard_grad_and_rmatmul(monkeypatch):
+    """the guard's per-batch route is autograd-safe (no ``out=``), and a ``tensor @
+    non-tensor`` product still reaches the other operand's __rmatmul__ inside the guard."""
+    from quantizers_amd import patching
+    monkeypatch.setattr(patching, "_ROUTE_DEVICES", ("cuda", "cpu"))
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 8, 768, generator=g).to(torch.bfloat16).requires_grad_(True)
+    nt = torch.randn(2, 4, 768, generator=g).to(torch.bfloat16).transpose(1, 2)
+
+    class R:
+        def __rmatmul__(self, other):
+            return "rmatmul"
+    with patching.bmm_guard():
+        y = torch.bmm(x, nt)
+        y.float().sum().backward()
+        assert x @ R() == "rmatmul"
+    assert x.grad is not None and x.grad.shape == x.shape
