@@ -55,6 +55,50 @@ from .recipe import AWQMapping
 log = logging.getLogger(__name__)
 
 PHASE_TIMING = os.environ.get("QZ_AWQ_PHASE_TIMING", "0") == "1"  # diagnostics: synchronised per-phase wall times
+
+# D8: the dtype of the AWQ statistics and grid scales.  "bf16" (default since round 5): SURVEY
+# A.6's reading of llmcompressor -- the running mean |x| kept in the activation dtype
+# ((prev_mean * prev_n + batch_sum) / n, every op rounded to bf16; the batch sum accumulated in
+# f32 and rounded once), w_mean a bf16 column sum per balance layer summed in bf16, the grid scale
+# formula evaluated in bf16, so W * s, Q(W*s)/s and the smoothing multiply by bf16 scales.  "fp32":
+# rounds 1-4 (x_mean f32 sums, w_mean f64 sums, scales f32).  On a 2-layer Qwen3-4B the two
+# readings differ in 3 of 6 argmins and 17.9 % of the packed int4 words (profiles/r05_d8_probe.txt),
+# so the choice is exposed (oneshot(awq_dtype=...), --awq-dtype).  The grid loss is an f64 sum of
+# f32(bf16(a - b))^2 in both (llmcompressor's f32 per-batch sum differs only in summation order).
+AWQ_DTYPES = ("bf16", "fp32")
+AWQ_DTYPE = "bf16"
+
+
+def _running_mean_bf16(parts) -> Optional[torch.Tensor]:
+    """llmcompressor's _accumulate_mean in bf16 over per-batch f32 sums [(sum [C], n), ...] in
+    batch order: m = s_0 / n_0, then m = (m * count + s_j) / (count + n_j)."""
+    m, c = None, 0
+    for part, n in parts:
+        if n == 0:
+            continue
+        sb = part.to(torch.bfloat16)
+        m = sb / n if m is None else (m * c + sb) / (c + n)
+        c += n
+    return m
+
+
+def _grid_scales_bf16(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo: bool,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """One grid point's scale vector(s) evaluated in bf16 as torch evaluates llmcompressor's
+    formula on bf16 statistics ([C] or a [B, C] stack of independent mappings): clamp(x^r /
+    (w^(1-r) + 1e-4), 1e-4) / sqrt(max * min), inf / nan -> 1.  Returned as f32 (exact bf16
+    values) for the kernels' column-scale arguments."""
+    xb = x_mean.to(torch.bfloat16)
+    if duo:
+        s = (xb.pow(ratio) / (w_mean.to(torch.bfloat16).pow(1 - ratio) + 1e-4)).clamp(min=1e-4)
+    else:
+        s = xb.pow(ratio).clamp(min=1e-4)
+    s = s / (s.amax(-1, keepdim=True) * s.amin(-1, keepdim=True)).sqrt()
+    s = torch.where(torch.isinf(s) | torch.isnan(s), torch.ones_like(s), s)
+    if out is None:
+        return s.float()
+    out.copy_(s)
+    return out
 PHASES: Dict[str, float] = {}  # phase name -> seconds, accumulated while PHASE_TIMING
 
 
@@ -295,11 +339,14 @@ class _ParentCache:
 
 
 class _AbsMean:
-    """Forward pre-hook on a balance layer: sum |x| per input channel (GPU kernel)."""
+    """Forward pre-hook on a balance layer: sum |x| per input channel (GPU kernel).  ``bf16``
+    (D8): every calibration batch's sum is kept apart and ``mean()`` is the bf16 running mean."""
 
-    def __init__(self, module: Optional[nn.Module] = None):
+    def __init__(self, module: Optional[nn.Module] = None, bf16: bool = False):
         self.sum = None
         self.count = 0
+        self.bf16 = bf16
+        self.parts: List[Tuple[torch.Tensor, int]] = []
         self.slots: Dict[int, List[Tuple[torch.Tensor, int]]] = {}
         self.h = module.register_forward_pre_hook(self._hook) if module is not None else None
 
@@ -318,6 +365,10 @@ class _AbsMean:
         in sample order gives the sequential calls' bits."""
         for j in sorted(self.slots):
             for part, n in self.slots[j]:
+                if self.bf16:
+                    self.parts.append((part, n))
+                    self.count += n
+                    continue
                 if self.sum is None:
                     self.sum = torch.zeros_like(part)
                 self.sum += part
@@ -325,12 +376,20 @@ class _AbsMean:
         self.slots = {}
 
     def add(self, x: torch.Tensor):
+        if self.bf16:  # one sum per calibration batch, combined by mean()
+            part = torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device)
+            n = ops.awq_absmean_accum(x.detach(), part) if x.numel() else 0
+            self.parts.append((part, n))
+            self.count += n
+            return
         if self.sum is None:
             self.sum = torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device)
         if x.numel():
             self.count += ops.awq_absmean_accum(x.detach(), self.sum)
 
     def mean(self) -> torch.Tensor:
+        if self.bf16:
+            return _running_mean_bf16(self.parts)
         return self.sum / max(self.count, 1)
 
     def remove(self):
@@ -643,6 +702,29 @@ def _group_size_for_mean(a: QuantizationArgs, cols: int) -> int:
     return cols
 
 
+def _w_mean(groups: List[List[LinearRef]], quantized: Dict[str, QuantizationArgs], cols: int, bf16: bool,
+            device) -> torch.Tensor:
+    """w_mean over the balance layers.  fp32 (D8 rounds 1-4): one f64 column sum over every row
+    of every balance layer, / rows, as f32.  bf16: llmcompressor's _compute_layer_means -- each
+    balance linear's column sum (f64 on the device, rounded to bf16), summed over the layers in
+    bf16, divided by the row count in bf16."""
+    if not bf16:
+        wsum = torch.zeros(cols, dtype=torch.float64, device=device)
+        rows = 0
+        for g in groups:
+            rows += ops.awq_weight_mean_accum(_view(g), _group_size_for_mean(quantized[g[0].name], cols), wsum)
+        return (wsum / rows).float()
+    acc, rows = None, 0
+    for g in groups:
+        gs = _group_size_for_mean(quantized[g[0].name], cols)
+        for ref in g:  # every balance linear is a layer of its own (each expert slice too)
+            part = torch.zeros(cols, dtype=torch.float64, device=device)
+            rows += ops.awq_weight_mean_accum(ref.weight, gs, part)
+            sb = part.to(torch.bfloat16)
+            acc = sb if acc is None else acc + sb
+    return acc / rows
+
+
 def _launch_groups(r: ResolvedMapping, quantized: Dict[str, QuantizationArgs]):
     """Balance refs grouped into single batched launches (same fused parameter, same scheme)."""
     out = []
@@ -803,7 +885,8 @@ def _expert_chunk(n_tokens: int, inter: int, hidden: int, budget: int = 4 << 30)
 def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dict]], mappings: List[AWQMapping],
               quantized: Dict[str, QuantizationArgs], duo_scaling: bool = True, n_grid: int = 20,
               mtype: str = "", calibrate_all_experts: bool = True,
-              stateful_observers: bool = False, batched_calls: bool = False) -> Dict[str, Any]:
+              stateful_observers: bool = False, batched_calls: bool = False,
+              awq_dtype: Optional[str] = None) -> Dict[str, Any]:
     """Run AWQ on one decoder layer in place.  ``layer_inputs`` are the cached (args, kwargs)
     of the layer for every calibration batch.  Returns per-mapping diagnostics.
 
@@ -812,7 +895,19 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     stateful reading); default: every observation is memoryless (D7).
     ``batched_calls``: run the calibration pass as one call over the stacked samples
     (``stack_layer_calls``; the hooks see the same per-sample inputs) -- the caller has checked
-    that the batched layer forward is bit-identical to the per-sample one."""
+    that the batched layer forward is bit-identical to the per-sample one.
+    ``awq_dtype``: "bf16" / "fp32" statistics and grid scales (D8, ``AWQ_DTYPE`` when None)."""
+    awq_dtype = AWQ_DTYPE if awq_dtype is None else awq_dtype
+    if awq_dtype not in AWQ_DTYPES:
+        raise ValueError(f"awq_dtype must be one of {AWQ_DTYPES}, got {awq_dtype!r}")
+    bf16 = awq_dtype == "bf16"
+
+    def grid_scales(xm, wm, ratio, out=None):
+        if bf16:
+            return _grid_scales_bf16(xm, wm, ratio, duo_scaling, out=out)
+        if xm.dim() == 2:
+            return ops.awq_grid_scales_batched(xm, wm, ratio, duo_scaling, out=out)
+        return ops.awq_grid_scales(xm, wm, ratio, duo_scaling, out=out)
     resolved = resolve_mappings(layer, prefix, mappings, quantized, mtype)
     if not resolved:
         return {}
@@ -824,7 +919,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
     for r in resolved:
         b0 = r.balance[0]
         if b0.index is None:
-            stats[r.smooth_name] = _AbsMean(b0.module)
+            stats[r.smooth_name] = _AbsMean(b0.module, bf16)
             hooks.append(stats[r.smooth_name])
         elif id(b0.module) not in experts:
             experts[id(b0.module)] = _ExpertInputs(b0.module, calibrate_all_experts)
@@ -865,7 +960,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             x_mean = stats[r.smooth_name].mean()
         else:
             ei = experts[id(b0.module)]
-            am = _AbsMean()
+            am = _AbsMean(bf16=bf16)
             for i in range(n_batches):
                 am.add(_virtual_input(ei, b0, i))
             if am.count == 0:  # expert never routed to (moe_calibrate_all_experts=False)
@@ -874,12 +969,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             x_mean = am.mean()
         groups = _launch_groups(r, quantized)
         # 2. w_mean over the balance layers (each with its own group size)
-        cols = b0.weight.shape[1]
-        wsum = torch.zeros(cols, dtype=torch.float64, device=x_mean.device)
-        rows = 0
-        for g in groups:
-            rows += ops.awq_weight_mean_accum(_view(g), _group_size_for_mean(quantized[g[0].name], cols), wsum)
-        w_mean = (wsum / rows).float()
+        w_mean = _w_mean(groups, quantized, b0.weight.shape[1], bf16, x_mean.device)
         # parent: forward closure over the calibration batches
         if r.parent_kind == "module":
             calls = caches[r.smooth_name].calls
@@ -920,7 +1010,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         # entry is an exact 0), so every rank sees the bit-identical history of one process
         orig = [_view(g).clone() for g in groups]
         tmp = [torch.empty_like(o) for o in orig]
-        scales = torch.empty_like(x_mean)
+        scales = torch.empty(x_mean.shape, dtype=torch.float32, device=x_mean.device)
         world, rank = _grid_ranks(grid_shard)
         obs = [(_ObserverState(quantized[g[0].name])
                 if stateful_observers and quantized[g[0].name].observer in STATEFUL_OBSERVERS else None)
@@ -933,7 +1023,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             run = graphed = _GraphedForward(run, r.smooth_name)
         for i in range(rank, n_grid, world):
             ratio = i / n_grid
-            ops.awq_grid_scales(x_mean, w_mean, ratio, duo_scaling, out=scales)
+            grid_scales(x_mean, w_mean, ratio, out=scales)
             for g, w0, t, o in zip(groups, orig, tmp, obs):
                 if o is not None:
                     _fake_quant_stateful(w0, quantized[g[0].name], scales, t, o)
@@ -956,7 +1046,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             raise RuntimeError(f"AWQ: no finite loss for {r.smooth_name} (history {history})")
         best, best_i = min(finite)  # first best ratio (strict <): min over (loss, index)
         best_ratio = best_i / n_grid
-        return best_ratio, best, history, ops.awq_grid_scales(x_mean, w_mean, best_ratio, duo_scaling)
+        return best_ratio, best, history, grid_scales(x_mean, w_mean, best_ratio)
 
     def apply(r: ResolvedMapping, found):
         """4. _apply_smoothing: balance columns *= s, smooth rows (and bias) /= s."""
@@ -998,12 +1088,15 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         hs = [torch.cat(h) if len(h) > 1 else h[0] for h in hid]  # all tokens of an expert: [T, I]
         del hid
         for k, ref in enumerate(refs):
-            am = _AbsMean()
-            am.add(hs[k])
+            am = _AbsMean(bf16=bf16)
+            if bf16:  # one sum per calibration batch: the batches' token runs of the expert
+                counts = [ei.tokens(i, ref.index[0]).shape[0] for i in range(n_batches)]
+                for piece in torch.split(hs[k], counts):
+                    am.add(piece)
+            else:
+                am.add(hs[k])
             xm[k] = am.mean()
-            wsum = torch.zeros(cols, dtype=torch.float64, device=w2.device)
-            rows = ops.awq_weight_mean_accum(ref.weight, _group_size_for_mean(a, cols), wsum)
-            wm[k] = (wsum / rows).float()
+            wm[k] = _w_mean([[ref]], quantized, cols, bf16, w2.device)
         # one GEMM per expert and grid point over all its tokens (2-D GEMMs: the path every
         # other mapping uses)
         w0 = torch.stack([w2[e] for e in es])  # [k, H, I] (pre-search weights)
@@ -1019,7 +1112,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             # Same GEMM and loss per (grid point, expert): bit-identical losses.
             wq_all = torch.empty((n_grid,) + tuple(w0.shape), dtype=w0.dtype, device=w0.device)
             for g in range(n_grid):
-                ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
+                grid_scales(xm, wm, g / n_grid, out=scales[g])
                 ops.fake_quantize_batched(w0, a, scales[g], out=wq_all[g])
             if OVERLAP_LOSS and w0.is_cuda:
                 _overlapped_losses(hs, ref_out, wq_all, losses)
@@ -1032,7 +1125,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             del wq_all
         else:
             for g in range(n_grid):
-                ops.awq_grid_scales_batched(xm, wm, g / n_grid, duo_scaling, out=scales[g])
+                grid_scales(xm, wm, g / n_grid, out=scales[g])
                 ops.fake_quantize_batched(w0, a, scales[g], out=wq)
                 for k, (h, ro) in enumerate(zip(hs, ref_out)):
                     ops.awq_sq_err_accum(ro, nn.functional.linear(h, wq[k]), losses[g, k:k + 1])

@@ -53,6 +53,9 @@ def parse_args(argv=None):
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--stateful-observers", action="store_true",
                    help="AWQ grid: minmax/static_minmax observers keep memory across grid points (DESIGN D7)")
+    p.add_argument("--awq-dtype", choices=("bf16", "fp32"), default=None,
+                   help="AWQ statistics / grid-scale dtype (DESIGN D8): bf16 = the activation dtype, as SURVEY "
+                        "A.6 reads llmcompressor (default); fp32 = rounds 1-4")
     p.add_argument("--placement", choices=("auto", "resident", "layerwise"), default="auto",
                    help="AWQ: keep a host-loaded model on the GPU (resident), onload one decoder layer at a "
                         "time (layerwise, the reference's placement), or resident when it fits in half "
@@ -180,7 +183,8 @@ def main(argv=None):
     oneshot(model=model, recipe=recipe_path, dataset=dataset, max_seq_length=max_len,
             num_calibration_samples=len(dataset) if dataset else None, moe_calibrate_all_experts=True,
             device=args.device, stateful_observers=args.stateful_observers,
-            device_resident={"auto": None, "resident": True, "layerwise": False}[args.placement])
+            device_resident={"auto": None, "resident": True, "layerwise": False}[args.placement],
+            awq_dtype=args.awq_dtype)
     logging.info("Completed quantization in %.2f seconds", time.time() - t0)
     if _rank() == 0:
         os.makedirs("outputs", exist_ok=True)

@@ -125,7 +125,7 @@ def _layer_out(o):
 @torch.no_grad()
 def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device, report,
                     calibrate_all_experts: bool = True, stateful_observers: bool = False, residency=None,
-                    seconds: Optional[List[float]] = None):
+                    seconds: Optional[List[float]] = None, awq_dtype: Optional[str] = None):
     """``seconds`` collects each layer's host wall time (as logged)."""
     seconds = [] if seconds is None else seconds
     layers = decoder_layers(model)
@@ -157,7 +157,7 @@ def _sequential_awq(model: nn.Module, awq: AWQModifier, schemes, batches, device
             batched = BATCH_LAYER_CALLS and _batched_forward_ok(layer, inputs)
         rep = awq_mod.awq_layer(layer, checkpoint_name(f"{lname}.{i}", mtype), inputs, mappings, weights,
                                 awq.duo_scaling, awq.n_grid, mtype=mtype, calibrate_all_experts=calibrate_all_experts,
-                                stateful_observers=stateful_observers, batched_calls=batched)
+                                stateful_observers=stateful_observers, batched_calls=batched, awq_dtype=awq_dtype)
         report[f"{lname}.{i}"] = rep
         stacked = awq_mod.stack_layer_calls(inputs) if batched else None
         with awq_mod.phase("propagation"):
@@ -184,7 +184,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
             moe_calibrate_all_experts: bool = True, device: Union[str, torch.device, None] = None,
             output_dir: Optional[str] = None, stateful_observers: bool = False,
             device_resident: Optional[bool] = None, max_shard_bytes: Optional[int] = None,
-            **kwargs) -> nn.Module:
+            awq_dtype: Optional[str] = None, **kwargs) -> nn.Module:
     """Apply the recipe to ``model`` in place (llmcompressor.oneshot signature as used at
     scripts/do_oneshot.py:179-187).  ``processor`` is accepted for API parity (unused: the
     dataset is already tokenized).  ``moe_calibrate_all_experts``: AWQ statistics and loss
@@ -197,6 +197,8 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     there (True), or only its decoder layers are onloaded one at a time and returned to the host
     (False, the reference's placement); default: resident when its parameters take at most
     half of the device's free memory.
+    ``awq_dtype``: "bf16" (default, SURVEY A.6's reading of llmcompressor: statistics and grid
+    scales in the activation dtype) or "fp32" (rounds 1-4) -- decision D8, awq.AWQ_DTYPE.
 
     Under torch.distributed with a meta-device skeleton on every rank but 0
     (``residency.Residency``, BASELINE configs[4]): rank 0's layers are broadcast as the pass
@@ -254,7 +256,7 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
                                "rotary embedding (rotary)": n_rot})
             for m in awqs:
                 _sequential_awq(model, m, schemes, batches, device, report, moe_calibrate_all_experts,
-                                stateful_observers, residency=res, seconds=layer_seconds)
+                                stateful_observers, residency=res, seconds=layer_seconds, awq_dtype=awq_dtype)
     elif res is not None:  # RTN: no calibration pass, but each rank still needs its shards' tensors
         stager = []
 

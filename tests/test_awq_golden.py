@@ -16,6 +16,7 @@ import ct_torch as ct
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FIX = os.path.join(ROOT, "tests", "golden", "awq_int4_g128.safetensors")
+FIX_BF16 = os.path.join(ROOT, "tests", "golden", "awq_int4_g128_bf16.safetensors")  # D8 bf16 reading
 OA = ct.QArgs(num_bits=4, type="int", symmetric=True, group_size=128)
 
 
@@ -30,14 +31,15 @@ def _bits_eq(a, b):
     assert torch.equal(a, b)
 
 
-def test_oracle_reproduces_awq_fixture():
+@pytest.mark.parametrize("literal", [False, True], ids=["fp32", "bf16"])
+def test_oracle_reproduces_awq_fixture(literal):
     import importlib.util
     spec = importlib.util.spec_from_file_location("make_awq_golden", os.path.join(ROOT, "tests", "golden",
                                                                                  "make_awq_golden.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    got = mod.build()
-    want = load_file(FIX)
+    got = mod.build(literal)
+    want = load_file(FIX_BF16 if literal else FIX)
     for k in ("x", "w", "x_mean", "w_mean", "scales", "best", "fq_best", "smoothed"):
         _bits_eq(got[k], want[k])
     torch.testing.assert_close(got["losses"], want["losses"], rtol=1e-9, atol=0)
@@ -79,4 +81,52 @@ def test_hip_awq_pipeline_matches_fixture(cuda):
     best = f["scales"][int(f["best"])].to(cuda)
     sm = w.clone()
     ops.scale_columns_(sm, best, divide=False)
+    _bits_eq(sm.cpu(), f["smoothed"])
+
+
+def _ulps_bf16(a, b):
+    """|a - b| in bf16 units of the last place (same-sign finite values)."""
+    return (a.view(torch.int16).to(torch.int32) - b.view(torch.int16).to(torch.int32)).abs()
+
+
+@pytest.mark.gpu
+def test_hip_awq_pipeline_matches_bf16_fixture(cuda):
+    """D8's bf16 reading through the product's own pieces (awq._AbsMean(bf16=True), awq._w_mean,
+    awq._grid_scales_bf16, the fake-quant and smoothing kernels with bf16 scales): statistics and
+    scale vectors within 1 bf16 ulp of the literal oracle (device vs CPU summation order / powf;
+    almost all equal), Q(W*s)/s and the smoothing bit for bit for the fixture's scales, the 20
+    losses to 2e-3 with the same argmin."""
+    from quantizers_amd import awq, ops
+    from quantizers_amd.model import LinearRef
+    from quantizers_amd.quantization import QuantizationArgs
+    f = load_file(FIX_BF16)
+    x, w = f["x"].to(cuda), f["w"].to(cuda)
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    am = awq._AbsMean(bf16=True)
+    am.add(x)
+    xm = am.mean()
+    assert xm.dtype == torch.bfloat16
+    d = _ulps_bf16(xm.cpu(), f["x_mean"])
+    assert d.max() <= 1 and (d > 0).float().mean() < 0.01, (int(d.max()), float((d > 0).float().mean()))
+    lin = torch.nn.Linear(w.shape[1], w.shape[0], bias=False, dtype=torch.bfloat16, device=cuda)
+    lin.weight.data = w
+    ref_lin = LinearRef("w", lin, "weight", None)
+    wm = awq._w_mean([[ref_lin]], {"w": a}, w.shape[1], True, cuda)
+    d = _ulps_bf16(wm.cpu(), f["w_mean"])
+    assert d.max() <= 1 and (d > 0).float().mean() < 0.01, (int(d.max()), float((d > 0).float().mean()))
+    ref = torch.nn.functional.linear(x, w)
+    losses = torch.zeros(20, dtype=torch.float64, device=cuda)
+    for i in range(20):
+        s = awq._grid_scales_bf16(f["x_mean"].to(cuda), f["w_mean"].to(cuda), i / 20, True)
+        d = _ulps_bf16(s.cpu().to(torch.bfloat16), f["scales"][i])
+        assert d.max() <= 1 and (d > 0).float().mean() < 0.01, (i, int(d.max()))
+        fq = ops.fake_quantize(w, a, col_scales=f["scales"][i].float().to(cuda))
+        if i == int(f["best"]):
+            _bits_eq(fq.cpu(), f["fq_best"])
+        ops.awq_sq_err_accum(ref, torch.nn.functional.linear(x, fq), losses[i:i + 1])
+    losses = losses.cpu() / ref.numel()
+    torch.testing.assert_close(losses, f["losses"], rtol=2e-3, atol=0)
+    assert int(torch.argmin(losses)) == int(f["best"])
+    sm = w.clone()
+    ops.scale_columns_(sm, f["scales"][int(f["best"])].float().to(cuda), divide=False)
     _bits_eq(sm.cpu(), f["smoothed"])

@@ -322,7 +322,8 @@ def test_dense_mlp_awq_all_ratios_and_argmin(cuda):
     norm0 = layer.post_attention_layernorm.weight.detach().clone()
     gw, uw = mlp0.gate_proj.weight.detach().cpu(), mlp0.up_proj.weight.detach().cpu()
     rep = awq_layer(layer, "model.layers.0", inputs,
-                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized)
+                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized,
+                    awq_dtype="fp32")
     r = rep["model.layers.0.post_attention_layernorm"]
     # restatement
     oa = ct.QArgs(group_size=128)
@@ -358,6 +359,73 @@ def test_dense_mlp_awq_all_ratios_and_argmin(cuda):
     _eq(layer.mlp.gate_proj.weight, (gw.float() * s.view(1, -1)).to(torch.bfloat16), "gate smoothed")
     _eq(layer.mlp.up_proj.weight, (uw.float() * s.view(1, -1)).to(torch.bfloat16), "up smoothed")
     _eq(layer.post_attention_layernorm.weight, (norm0.cpu().float() / s).to(torch.bfloat16), "norm smoothed")
+
+
+def test_dense_mlp_awq_bf16_matches_literal_oracle(cuda):
+    """D8, bf16 reading (the default since round 5): post_attention_layernorm -> {gate, up} through
+    awq_layer vs the literal restatement (ct_torch.*_literal: the bf16 running mean over the
+    calibration batches, bf16 w_mean per layer, bf16 grid formula, Q(W*s)/s with bf16 scales): all
+    20 losses, the argmin, and the applied smoothing -- bf16(W * s) on gate / up and bf16(w / s) on
+    the norm with the product's own bf16 scale vector (itself within 1 ulp of the restatement's)."""
+    import copy
+    from quantizers_amd import awq as awq_mod
+    from quantizers_amd.awq import awq_layer
+    from quantizers_amd.oneshot import _batches, _capture_layer0_inputs
+    from quantizers_amd.quantization import QuantizationArgs
+    from quantizers_amd.recipe import AWQMapping
+    m = _qwen3(layers=1).to(cuda)
+    layer = m.model.layers[0]
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    quantized = {f"model.layers.0.mlp.{p}": a for p in ("gate_proj", "up_proj", "down_proj")}
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(_calib(n=3, s=64), None, None, cuda))
+    xs = []
+    h = layer.mlp.register_forward_pre_hook(lambda mod, args: xs.append(args[0].detach().clone()))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    mlp0 = copy.deepcopy(layer.mlp)
+    norm0 = layer.post_attention_layernorm.weight.detach().clone()
+    gw, uw = mlp0.gate_proj.weight.detach().cpu(), mlp0.up_proj.weight.detach().cpu()
+    rep = awq_layer(layer, "model.layers.0", inputs,
+                    [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized,
+                    awq_dtype="bf16")
+    r = rep["model.layers.0.post_attention_layernorm"]
+    oa = ct.QArgs(group_size=128)
+    prev = None
+    for x in xs:
+        prev = ct.awq_accumulate_mean_literal(x.cpu().reshape(-1, x.shape[-1]), prev)
+    x_mean = prev[0]
+    w_mean = ct.awq_layer_means_literal([gw, uw], oa)
+    xcat = torch.cat([x.reshape(-1, x.shape[-1]) for x in xs])
+    with torch.no_grad():
+        ref_out = mlp0(xcat)
+        hist = []
+        probe = copy.deepcopy(mlp0)
+        for i in range(20):
+            s = ct.awq_grid_scales_literal(x_mean, w_mean, i / 20, True)
+            probe.gate_proj.weight.copy_(ct.awq_fake_quant_scaled_literal(gw, s, oa))
+            probe.up_proj.weight.copy_(ct.awq_fake_quant_scaled_literal(uw, s, oa))
+            hist.append((ref_out - probe(xcat)).double().pow(2).sum().item() / ref_out.numel())
+    torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(hist), rtol=5e-3, atol=1e-12)
+    best_i = int(round(r["best_ratio"] * 20))
+    assert hist[best_i] <= min(hist) * 1.005
+    # the product's own statistics (bf16) -> its scale vector; within 1 ulp of the restatement's
+    am = awq_mod._AbsMean(bf16=True)
+    for x in xs:
+        am.add(x)
+    parts = []
+    for w_ in (gw, uw):
+        ws_ = torch.zeros(w_.shape[1], dtype=torch.float64, device=cuda)
+        parts.append((ws_, ops.awq_weight_mean_accum(w_.to(cuda), 128, ws_)))
+    wm_dev = (parts[0][0].to(torch.bfloat16) + parts[1][0].to(torch.bfloat16)) / (parts[0][1] + parts[1][1])
+    s_dev = awq_mod._grid_scales_bf16(am.mean(), wm_dev, best_i / 20, True).cpu()
+    s_lit = ct.awq_grid_scales_literal(x_mean, w_mean, best_i / 20, True)
+    d = (s_dev.to(torch.bfloat16).view(torch.int16).int() - s_lit.view(torch.int16).int()).abs()
+    assert d.max() <= 1 and (d > 0).float().mean() < 0.02, (int(d.max()), float((d > 0).float().mean()))
+    _eq(layer.mlp.gate_proj.weight, (gw.float() * s_dev.view(1, -1)).to(torch.bfloat16), "gate smoothed")
+    _eq(layer.mlp.up_proj.weight, (uw.float() * s_dev.view(1, -1)).to(torch.bfloat16), "up smoothed")
+    _eq(layer.post_attention_layernorm.weight, (norm0.cpu().float() / s_dev).to(torch.bfloat16), "norm smoothed")
 
 
 @pytest.mark.parametrize("observer", ["minmax", "static_minmax"])
@@ -410,7 +478,7 @@ def test_stateful_observer_grid(cuda, observer):
     gw, uw = mlp0.gate_proj.weight.detach().cpu(), mlp0.up_proj.weight.detach().cpu()
     rep = awq_layer(layer, "model.layers.0", inputs,
                     [AWQMapping("re:.*post_attention_layernorm$", ["re:.*gate_proj$", "re:.*up_proj$"])], quantized,
-                    stateful_observers=True)
+                    stateful_observers=True, awq_dtype="fp32")
     r = rep["model.layers.0.post_attention_layernorm"]
     sums = torch.zeros(gw.shape[1], dtype=torch.float32, device=cuda)
     cnt = sum(ops.awq_absmean_accum(x, sums) for x in xs)
@@ -622,7 +690,7 @@ def test_expert_w3_w2_awq_matches_oracle(cuda, calibrate_all):
     h.remove()
     gu0, down0 = experts.gate_up_proj.data.clone(), experts.down_proj.data.clone()
     rep = awq_layer(layer, "model.layers.0", inputs, [AWQMapping("re:.*w3$", ["re:.*w2$"])], quantized,
-                    mtype="minimax_m2", calibrate_all_experts=calibrate_all)
+                    mtype="minimax_m2", calibrate_all_experts=calibrate_all, awq_dtype="fp32")
     assert len(rep) == 4
     oa = ct.QArgs(group_size=32)
     for e in range(4):
