@@ -23,7 +23,7 @@
 using namespace qz;
 
 #ifndef QZ_BLK_NB
-#define QZ_BLK_NB 4  // widest strip (blocks per workgroup); the host takes the widest that divides cols/128
+#define QZ_BLK_NB 2  // widest strip (blocks per workgroup); the host takes the widest that divides cols/128
 #endif
 #ifndef QZ_BLK_LD
 #define QZ_BLK_LD 2  // weight loads: 0 = default policy, 2 = non-temporal

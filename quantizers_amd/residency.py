@@ -110,6 +110,8 @@ def broadcast_slots(ss: List[Slot], device, src: int = 0) -> None:
     ``src`` holds one shared tensor on the other ranks too (``src``'s alias structure is sent
     along), so ties survive on every rank and no rank's checkpoint gains an untied copy."""
     world, rank = _world()
+    if world == 1:  # no other rank to send to: src's tensors are already in place
+        return
     alias = _alias_groups(ss) if rank == src else None
     if world > 1:
         box = [alias]

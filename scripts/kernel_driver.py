@@ -70,6 +70,20 @@ def main(n=30):
         ("nvfp4_fused", lambda i: ops.quantize_weight(gus[i % 4][:, :768], nv, out=nv_out), 1),
         ("nvfp4_two_pass", nv_two_pass, 1),
     ]
+    # FP8_BLOCK 128x128 (BASELINE configs[2], the mixed recipe's attention half): the strip kernel
+    # as CompressionPlan issues it -- grouped launches over the Qwen3-4B k+v (72 x [1024, 2560]) and
+    # q (36 x [4096, 2560]) weights -- and one batch launch over a [36, 1024, 2560] stack
+    fb = QuantizationArgs(num_bits=8, type="float", strategy="block", block_structure=[128, 128])
+    kv = [(torch.randn(1024, 2560, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for _ in range(72)]
+    qw = [(torch.randn(4096, 2560, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for _ in range(36)]
+    g_kv, g_q = ops.GroupedQuantize(kv, fb), ops.GroupedQuantize(qw, fb)
+    stk = (torch.randn(36, 1024, 2560, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
+    stk_out = ops.alloc_outputs(tuple(stk.shape), fb, None, dev)
+    kernels += [
+        ("fp8_block_grouped_kv", lambda i: g_kv.run(), 1),
+        ("fp8_block_grouped_q", lambda i: g_q.run(), 1),
+        ("fp8_block_stack_kv", lambda i: ops.quantize_weight(stk, fb, out=stk_out), 1),
+    ]
     st = torch.cuda.current_stream()
     for name, fn, _ in kernels:
         for i in range(3):

@@ -47,6 +47,13 @@ KERNELS = {
     "k_group_fast<1, 3, false, true, true, false>": ("NVFP4 two-pass quantize pass [128, 768, 2048]",
                                                      int(128 * 768 * 2048 * (2 + 0.5 + 1 / 16)) + 128 * 4),
     "k_absmax_slices": ("NVFP4 two-pass per-slice |w| max pre-pass [128, 768, 2048]", 128 * 768 * 2048 * 2),
+    # FP8_BLOCK 128x128 (round 5, qz_block.hip): read 2 B + e4m3 1 B per param + a bf16 scale per block;
+    # kernel_driver runs the table-mode kernel in two legs, k+v then q
+    "k_block_fp8<2, true>#0": ("FP8_BLOCK grouped launch 72 x [1024, 2560] (Qwen3-4B k+v)",
+                               72 * 1024 * 2560 * 3 + 72 * 8 * 20 * 2),
+    "k_block_fp8<2, true>#1": ("FP8_BLOCK grouped launch 36 x [4096, 2560] (Qwen3-4B q)",
+                               36 * 4096 * 2560 * 3 + 36 * 32 * 20 * 2),
+    "k_block_fp8<2, false>": ("FP8_BLOCK batch launch [36, 1024, 2560]", 36 * 1024 * 2560 * 3 + 36 * 8 * 20 * 2),
 }
 
 
