@@ -703,11 +703,12 @@ def _group_size_for_mean(a: QuantizationArgs, cols: int) -> int:
 
 
 def _w_mean(groups: List[List[LinearRef]], quantized: Dict[str, QuantizationArgs], cols: int, bf16: bool,
-            device) -> torch.Tensor:
+            device, refs: Optional[List[LinearRef]] = None) -> torch.Tensor:
     """w_mean over the balance layers.  fp32 (D8 rounds 1-4): one f64 column sum over every row
     of every balance layer, / rows, as f32.  bf16: llmcompressor's _compute_layer_means -- each
     balance linear's column sum (f64 on the device, rounded to bf16), summed over the layers in
-    bf16, divided by the row count in bf16."""
+    bf16 in the mapping's balance order (``refs``; the module order llmcompressor iterates),
+    divided by the row count in bf16."""
     if not bf16:
         wsum = torch.zeros(cols, dtype=torch.float64, device=device)
         rows = 0
@@ -715,13 +716,12 @@ def _w_mean(groups: List[List[LinearRef]], quantized: Dict[str, QuantizationArgs
             rows += ops.awq_weight_mean_accum(_view(g), _group_size_for_mean(quantized[g[0].name], cols), wsum)
         return (wsum / rows).float()
     acc, rows = None, 0
-    for g in groups:
-        gs = _group_size_for_mean(quantized[g[0].name], cols)
-        for ref in g:  # every balance linear is a layer of its own (each expert slice too)
-            part = torch.zeros(cols, dtype=torch.float64, device=device)
-            rows += ops.awq_weight_mean_accum(ref.weight, gs, part)
-            sb = part.to(torch.bfloat16)
-            acc = sb if acc is None else acc + sb
+    for ref in (refs if refs is not None else [x for g in groups for x in g]):
+        # every balance linear is a layer of its own (each expert slice too)
+        part = torch.zeros(cols, dtype=torch.float64, device=device)
+        rows += ops.awq_weight_mean_accum(ref.weight, _group_size_for_mean(quantized[ref.name], cols), part)
+        sb = part.to(torch.bfloat16)
+        acc = sb if acc is None else acc + sb
     return acc / rows
 
 
@@ -969,7 +969,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             x_mean = am.mean()
         groups = _launch_groups(r, quantized)
         # 2. w_mean over the balance layers (each with its own group size)
-        w_mean = _w_mean(groups, quantized, b0.weight.shape[1], bf16, x_mean.device)
+        w_mean = _w_mean(groups, quantized, b0.weight.shape[1], bf16, x_mean.device, r.balance)
         # parent: forward closure over the calibration batches
         if r.parent_kind == "module":
             calls = caches[r.smooth_name].calls

@@ -687,6 +687,25 @@ def test_fp8_block_batch_and_zero_blocks(cuda):
     assert got["scale"][1, 0, 0].float().item() == 0.0078125 and not got["codes"][1, :128, :128].view(torch.uint8).any()
 
 
+def test_fp8_block_store_policies_agree(cuda):
+    """The strip kernel writes its codes write-through (sc1) in launches moving < 768 MiB and
+    non-temporally above: a [9, 8192, 4096] batch (906 MB moved, nt stores) == its nine per-slice
+    launches (135 MB each, sc1 stores), and slice 4 == the plain-C oracle."""
+    import qref
+    a = QuantizationArgs(**FP8_BLOCK)
+    g = torch.Generator(device=cuda).manual_seed(14)
+    w = (torch.randn(9, 8192, 4096, device=cuda, generator=g) * 0.02).to(torch.bfloat16)
+    assert w.numel() * 3 > 768 << 20 and w[0].numel() * 3 < 768 << 20
+    big = ops.quantize_weight(w, a)
+    for e in range(9):
+        one = ops.quantize_weight(w[e], a)
+        _eq(big["codes"][e], one["codes"])
+        _eq(big["scale"][e], one["scale"])
+    want = qref.compress_weight(w[4].cpu(), _oracle_args(a))
+    _eq(big["codes"][4], want["weight"])
+    _eq(big["scale"][4], want["weight_scale"])
+
+
 @pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "int8_g64_sym", "fp8_g32", "mxfp4_g32",
                                     "fp8_block128"])
 def test_quantize_grouped_equals_single_calls(cuda, scheme):
