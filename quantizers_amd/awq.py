@@ -54,7 +54,7 @@ from .recipe import AWQMapping
 
 log = logging.getLogger(__name__)
 
-PHASE_TIMING = os.environ.get("QZ_AWQ_PHASE_TIMING", "0") == "1"  # diagnostics: synchronised per-phase wall times
+PHASE_TIMING = False  # diagnostics (set True): synchronised per-phase wall times, logged per layer
 
 # D8: the dtype of the AWQ statistics and grid scales.  "bf16" (default since round 5): SURVEY
 # A.6's reading of llmcompressor -- the running mean |x| kept in the activation dtype

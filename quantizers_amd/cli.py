@@ -109,9 +109,9 @@ def load_model(args, run):
     """The model in bf16 on the host (do_oneshot.py:86-94).  Under torchrun only rank 0 loads the
     weights; the other ranks build a meta-device skeleton of the same architecture and receive
     each decoder layer by broadcast as the AWQ pass reaches it (``residency``): one host copy
-    of the model for the whole job (QZ_RANK_COPIES=1 restores one copy per rank)."""
+    of the model for the whole job (RANK_COPIES = True restores one copy per rank)."""
     from transformers import AutoConfig, AutoModelForCausalLM
-    if _rank() != 0 and os.environ.get("QZ_RANK_COPIES", "0") != "1":
+    if _rank() != 0 and not RANK_COPIES:
         cfg = AutoConfig.from_pretrained(args.random_init or args.model_path or run.model.name, trust_remote_code=True)
         with torch.device("meta"):
             return AutoModelForCausalLM.from_config(cfg, dtype=torch.bfloat16)

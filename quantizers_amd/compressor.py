@@ -355,7 +355,7 @@ def _dist_info() -> Tuple[int, int]:
 
 
 STAGE_BYTES = 4 << 30  # host-resident weights staged on the device per plan
-WRITE_THREADS = int(os.environ.get("QZ_WRITE_THREADS", "4"))  # concurrent shard-file writers
+WRITE_THREADS = 4  # concurrent shard-file writers
 
 
 def _compress_chunks(units: Sequence[CompressUnit], device, copier: Optional["_HostCopier"], timings: Dict[str, float]):

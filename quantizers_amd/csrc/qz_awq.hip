@@ -36,18 +36,10 @@ int launch_err() {
 // rows past the chunk end are skipped by a wave-uniform branch.  The SWP wave sums are added in a
 // fixed order (((s0 + s1) + s2) + ...) through LDS -> part[chunk][c]; stage 2 (k_colsum_final)
 // adds the chunks in a fixed order: deterministic.
-#ifndef QZ_ABSMEAN_WPB
-#define QZ_ABSMEAN_WPB 8  // tuning knob: waves per absmean stage-1 workgroup
-#endif
-#ifndef QZ_WMEAN_WPB
-#define QZ_WMEAN_WPB 8  // tuning knob: waves per w_mean stage-1 workgroup
-#endif
-#ifndef QZ_ABSMEAN_NB
-#define QZ_ABSMEAN_NB 8  // tuning knob: activation rows per batch (loads in flight per lane)
-#endif
-#ifndef QZ_WMEAN_NB
-#define QZ_WMEAN_NB 4  // tuning knob: weight rows per batch (f64 sums: fewer, to keep VGPRs < 128)
-#endif
+constexpr int QZ_ABSMEAN_WPB = 8; // waves per absmean stage-1 workgroup
+constexpr int QZ_WMEAN_WPB = 8; // waves per w_mean stage-1 workgroup
+constexpr int QZ_ABSMEAN_NB = 8; // activation rows per batch (loads in flight per lane)
+constexpr int QZ_WMEAN_NB = 4; // weight rows per batch (f64 sums: fewer, to keep VGPRs < 128)
 constexpr int AWP = QZ_ABSMEAN_WPB, WWP = QZ_WMEAN_WPB;
 
 // walk rows r0 + wv, r0 + wv + SWP, ... < r1 of the 8 columns at col (clamped into [0, C - 8]);
@@ -163,49 +155,25 @@ __global__ __launch_bounds__(FW * 64) void k_colsum_final(const T* part, int64_t
 constexpr int STATS_CNT = 8192;  // arrival counters (uint32) at the head of a statistics workspace
 constexpr int64_t STATS_HEAD = (int64_t)STATS_CNT * 4;
 static_assert(STATS_HEAD == QZ_STATS_HEAD_BYTES, "counter head of the statistics workspace (quantizers_amd.h)");
-#ifndef QZ_STATS_CPG
-#define QZ_STATS_CPG 32  // tuning knob: chunks per first-level reduction group
-#endif
-#ifndef QZ_ABS1_WIN
-#define QZ_ABS1_WIN 128  // tuning knob: absmean column window (128 / 256 / 512)
-#endif
-#ifndef QZ_ABS1_WPB
-#define QZ_ABS1_WPB 8
-#endif
-#ifndef QZ_ABS1_NB
-#define QZ_ABS1_NB 16  // rows per lane per walk batch ([16384, 4096]: a whole 512-token chunk in flight;
+constexpr int QZ_STATS_CPG = 32; // chunks per first-level reduction group
+constexpr int QZ_ABS1_WIN = 128; // absmean column window (128 / 256 / 512)
+constexpr int QZ_ABS1_WPB = 8;
+constexpr int QZ_ABS1_NB = 16; // rows per lane per walk batch ([16384, 4096]: a whole 512-token chunk in flight;
                         // 24.79 -> 24.35 us back to back, same bits: profiles/r04aj_tune_stats.log)
-#endif
-#ifndef QZ_ABS1_BLOCKS
-#define QZ_ABS1_BLOCKS 1024  // tuning knob: target workgroups of the one-launch absmean
-#endif
-#ifndef QZ_ABS1_MIN_RC
-#define QZ_ABS1_MIN_RC 256  // tuning knob: minimum tokens per chunk
-#endif
-#ifndef QZ_WM1_WIN
-#define QZ_WM1_WIN 128  // tuning knob: w_mean column window (at least the group size)
-#endif
-#ifndef QZ_WM1_WPB
-#define QZ_WM1_WPB 8
-#endif
-#ifndef QZ_WM1_NB
-#define QZ_WM1_NB 4
-#endif
-#ifndef QZ_WM1_BLOCKS
-#define QZ_WM1_BLOCKS 256  // tuning knob: target workgroups of the one-launch w_mean
-#endif
-#ifndef QZ_WM1_MIN_RC
-#define QZ_WM1_MIN_RC 128  // tuning knob: minimum rows per chunk
-#endif
+constexpr int QZ_ABS1_BLOCKS = 1024; // target workgroups of the one-launch absmean
+constexpr int QZ_ABS1_MIN_RC = 256; // minimum tokens per chunk
+constexpr int QZ_WM1_WIN = 128; // w_mean column window (at least the group size)
+constexpr int QZ_WM1_WPB = 8;
+constexpr int QZ_WM1_NB = 4;
+constexpr int QZ_WM1_BLOCKS = 256; // target workgroups of the one-launch w_mean
+constexpr int QZ_WM1_MIN_RC = 128; // minimum rows per chunk
 
 // rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per
 // batch, the next batch loaded before the current one is used; f(v, valid) per row in order.  rb
 // is wave-uniform; every row of a batch that is followed by another batch is valid.  (Two
 // register sets used in turn instead of the copy measured the same time with more VGPRs.)
-#ifndef QZ_STATS_NT
-#define QZ_STATS_NT 1  // non-temporal 16-B loads in the one-launch statistics walk: absmean 26.2 -> 25.0 us,
+constexpr int QZ_STATS_NT = 1; // non-temporal 16-B loads in the one-launch statistics walk: absmean 26.2 -> 25.0 us,
                         // w_mean 19.4 -> 18.1 us back to back, same bits (profiles/r04d_tune_stats.log)
-#endif
 template <int S, int SNB, typename F>
 __device__ __forceinline__ void stats_walk(const uint16_t* base, int64_t ld, int64_t rb, int q, int64_t r1, F&& f) {
   if (rb >= r1) return;
@@ -527,12 +495,8 @@ int64_t sqdiff_blocks(int64_t rows, int64_t cols) {
   return std::max<int64_t>(1, std::min<int64_t>(2048, cdiv(rows * cols, 256 * 8 * 4)));
 }
 
-#ifndef QZ_ABSMEAN_MIN_TC
-#define QZ_ABSMEAN_MIN_TC 128  // tuning knob: minimum tokens per stage-1 chunk
-#endif
-#ifndef QZ_ABSMEAN_BLOCKS
-#define QZ_ABSMEAN_BLOCKS 1024  // tuning knob: target stage-1 workgroups
-#endif
+constexpr int QZ_ABSMEAN_MIN_TC = 128; // minimum tokens per stage-1 chunk
+constexpr int QZ_ABSMEAN_BLOCKS = 1024; // target stage-1 workgroups
 int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
   // >= QZ_ABSMEAN_MIN_TC tokens per chunk (32 per wave: one round of 8 loads); about
   // QZ_ABSMEAN_BLOCKS stage-1 blocks
@@ -542,12 +506,8 @@ int64_t absmean_chunks(int64_t T, int64_t C, int64_t* tc) {
   return cdiv(T, *tc);
 }
 
-#ifndef QZ_WMEAN_BLOCKS
-#define QZ_WMEAN_BLOCKS 256  // tuning knob: target stage-1 workgroups of w_mean
-#endif
-#ifndef QZ_WMEAN_MIN_RC
-#define QZ_WMEAN_MIN_RC 16  // tuning knob: minimum rows per stage-1 chunk
-#endif
+constexpr int QZ_WMEAN_BLOCKS = 256; // target stage-1 workgroups of w_mean
+constexpr int QZ_WMEAN_MIN_RC = 16; // minimum rows per stage-1 chunk
 // row chunks of the w_mean stage 1: >= QZ_WMEAN_MIN_RC rows each, about QZ_WMEAN_BLOCKS workgroups
 int64_t wmean_chunks(int64_t R, int64_t C, int64_t* rc) {
   const int64_t bx = cdiv(C, 512);

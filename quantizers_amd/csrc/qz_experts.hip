@@ -47,13 +47,6 @@ struct LtApi {
   bool ok = false;
 };
 
-bool debug() {
-  static const bool d = [] {
-    const char* e = getenv("QZ_EXPERT_GEMMS_DEBUG");
-    return e && *e == '1';
-  }();
-  return d;
-}
 
 // Which hipBLASLt: the copy already mapped into the process (PyTorch loads its bundled
 // libhipblaslt.so as a dependency of libtorch_hip, RTLD_LOCAL, so it is not visible through
@@ -106,7 +99,6 @@ int bind(const char* path) {
   g_lib = h;
   g_bound = true;
   g_status = std::string("bound: ") + path;
-  if (debug()) fprintf(stderr, "qz_expert_gemms: %s\n", g_status.c_str());
   return QZ_OK;
 }
 

@@ -300,7 +300,7 @@ def _log_swaps(model: nn.Module, counts: Dict[str, int]) -> None:
             log.info("AWQ pass: %s swap not applicable to model type %s", name, mtype)
 
 
-WARMUP = os.environ.get("QZ_WARMUP", "1") == "1"  # first-call library set-up on a thread beside the model move
+WARMUP = True  # first-call library set-up on a thread beside the model move
 
 
 def _start_warmup(model: nn.Module, device, seq_len: int) -> Optional[threading.Thread]:
@@ -330,7 +330,7 @@ def _start_warmup(model: nn.Module, device, seq_len: int) -> Optional[threading.
 
 
 BATCH_LAYER_CALLS = os.environ.get("QZ_BATCH_LAYER_CALLS", "1") == "1"
-HOST_COPY = os.environ.get("QZ_HOST_COPY", "keep")  # host image of a moved model: kept with the model / "release"d
+HOST_COPY = "keep"  # host image of a moved model: kept with the model / "release"d (r03ae A/B)
 
 
 @torch.no_grad()
@@ -388,7 +388,7 @@ def _to_device_staged(model: nn.Module, device) -> None:
     # synchronise waited 0.69 s on an idle device and the layer-0 capture took 0.95 s instead of
     # 0.28 s (QZ_AWQ_PHASE_TIMING=1, scripts/gpu_r03ad.sh).  So the host image is kept with the
     # model (the reference's model lives on the host throughout anyway) and goes when the model
-    # does; QZ_HOST_COPY=release frees it on a helper thread instead, one tensor at a time.
+    # does; HOST_COPY = "release" frees it on a helper thread instead, one tensor at a time.
     if HOST_COPY == "release":
         def release():
             while old:

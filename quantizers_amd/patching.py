@@ -73,14 +73,14 @@ def _per_batch_mm(a, b):
     return out.reshape(*lead, a.shape[-2], b.shape[-1])
 
 
-BMM_GUARD = os.environ.get("QZ_BMM_GUARD", "1") == "1"
+BMM_GUARD = True
 
 
 @contextlib.contextmanager
 def bmm_guard():
     """torch.bmm / torch.matmul / Tensor.matmul / Tensor.__matmul__ with the pinned defect's
     operands go through ``_per_batch_mm`` inside the context; everything else is untouched.
-    ``QZ_BMM_GUARD=0`` leaves torch as it is (A/B knob)."""
+    ``BMM_GUARD = False`` leaves torch as it is."""
     if not BMM_GUARD:
         yield
         return
