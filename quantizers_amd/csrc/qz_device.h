@@ -45,6 +45,31 @@ __device__ __forceinline__ void st16_wt(void* p, const uint4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
 }
 
+// Output stores of the streaming quantize kernels: non-temporal through most of a launch, but the
+// workgroups that write the launch's LAST QZ_WT_TAIL_BYTES of outputs store write-through (sc1,
+// 16 B per lane): a non-temporal store leaves its line dirty in the XCD's L2, and what is still
+// dirty when the launch ends is written back by the end-of-kernel release, on the critical path
+// (MI355X_MICROARCH.md price list, "boundary": + bytes / 6 TB/s); write-through stores all the way
+// cost 2-4 % on multi-GB launches (profiles/r05d_tune_plan.log).  Workgroups are ranked by linear
+// id (blockIdx.y * gridDim.x + blockIdx.x), the order they are dispatched in.  The int4 group path
+// takes a 32 MiB tail: the whole-model plan (5 launches) 1366.0 -> 1358.0 us; 64 / 128 / 256 MiB
+// tails and whole launches were slower in the plan although faster launch by launch in isolation
+// (profiles/r05e_tune_plan.log, r05f_tune_plan.log).  The FP8_BLOCK strip kernel takes none
+// (qz_block.hip).
+#ifndef QZ_WT_TAIL_BYTES
+#define QZ_WT_TAIL_BYTES (32ll << 20)
+#endif
+__device__ __forceinline__ bool wt_tail(uint32_t wt_from) {
+  return blockIdx.y * gridDim.x + blockIdx.x >= wt_from;
+}
+// first workgroup of the write-through tail of a launch of `wgs` workgroups writing `out_bytes`
+inline uint32_t wt_tail_from(int64_t wgs, int64_t out_bytes, int64_t tail_bytes = QZ_WT_TAIL_BYTES) {
+  if (wgs <= 0 || out_bytes <= 0 || wgs >= 0xffffffffll) return 0xffffffffu;
+  const int64_t per = (out_bytes + wgs - 1) / wgs;
+  const int64_t tail = (tail_bytes + per - 1) / per;
+  return (uint32_t)(tail >= wgs ? 0 : wgs - tail);
+}
+
 // torch.clamp: NaN propagates
 __device__ __forceinline__ float clamp_t(float x, float lo, float hi) {
   return (x != x) ? x : fminf(fmaxf(x, lo), hi);

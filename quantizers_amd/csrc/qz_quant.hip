@@ -62,6 +62,8 @@ struct FastArgs {
   QP p;
   int out_fmt;
   int scale_bytes;  // 2 (bf16) or 1 (e4m3 / e8m0)
+  uint32_t wt_from;  // nt int4 path: workgroups from this linear id on store a lane quad's codes as one
+                     // 16-B write-through store (wt_tail; 0xffffffff = never; every slice a multiple of 4 units)
   void* q_out;
   void* s_out;
   int8_t* zp_out;
@@ -278,7 +280,18 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       const uint32_t e_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].x), __float_as_uint(q[2].x), 0x04000c0cu);
       const uint32_t o_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].y), __float_as_uint(q[0].y), 0x0c0c0400u);
       const uint32_t o_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].y), __float_as_uint(q[2].y), 0x04000c0cu);
-      st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, ((o_lo | o_hi) << 4) | (e_lo | e_hi));
+      const uint32_t word = ((o_lo | o_hi) << 4) | (e_lo | e_hi);
+      if (NTS && wt_tail(A.wt_from)) {
+        // the 4 words of a lane quad (4 consecutive units of one slice: 16 contiguous bytes; the
+        // host sets wt only when every slice holds a multiple of 4 units, so a quad is valid as a
+        // whole) gathered into its first lane by DPP quad broadcasts, one 16-B write-through store
+        const uint32_t w1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0x55, 0xF, 0xF, true);
+        const uint32_t w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xAA, 0xF, 0xF, true);
+        const uint32_t w3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xFF, 0xF, 0xF, true);
+        if ((__lane_id() & 3) == 0) st16_wt(reinterpret_cast<uint32_t*>(A.q_out) + unit, make_uint4(word, w1, w2, w3));
+      } else {
+        st_out<NTS>(reinterpret_cast<uint32_t*>(A.q_out) + unit, word);
+      }
     } else {
       uint32_t c[8];
 #pragma unroll
@@ -1611,6 +1624,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     F.tab = nullptr;
     F.n_tab = 0;
     F.n_seg = 0;
+    F.wt_from = 0xffffffffu;  // set with the grid below
     int logl = 0;
     while ((8 << logl) < g) ++logl;
     const bool nt = batch * rows * cols * 2 > (fq ? QZ_NT_BYTES : QZ_NT_BYTES_Q);
@@ -1623,6 +1637,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     }
     const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(fq, nt) * WAVE);
     const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
+    if (!fq && pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits == 4 && F.units_per_batch % 4 == 0)
+      F.wt_from = wt_tail_from(blocks * batch, batch * F.units_per_batch * 4);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
                        dim3(FBLOCK), 0, st, F);
     return launch_err();
@@ -1664,6 +1680,7 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
       F.tab = nullptr;
       F.n_tab = 0;
       F.n_seg = 0;
+      F.wt_from = 0xffffffffu;
       TileArgs T;
       T.rows = rows;
       T.tile_rows = th;
@@ -1757,11 +1774,14 @@ int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t 
   F.tab = table;
   F.n_tab = n;
   F.n_seg = 0;
+  F.wt_from = 0xffffffffu;
   int logl = 0;
   while ((8 << logl) < g) ++logl;
   const bool nt = n * rows * cols * 2 > QZ_NT_BYTES_Q;
   const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(false, nt) * WAVE);
   const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
+  if (pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits == 4 && F.units_per_batch % 4 == 0)
+    F.wt_from = wt_tail_from(blocks * n, n * F.units_per_batch * 4);
   hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, nt, true), dim3((unsigned)blocks, (unsigned)n),
                      dim3(FBLOCK), 0, (hipStream_t)stream, F);
   return launch_err();
@@ -1827,6 +1847,11 @@ int qz_quantize_grouped_var(int64_t n, const uint64_t* table, const int64_t* row
   F.cs_ld_batch = 0;
   F.tab = table;
   F.n_tab = n;
+  bool wt_ok = pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits == 4;
+  int64_t units = 0;
+  for (int i = 0; i < n; ++i) units += rows[i] * cols[i] / 8;
+  for (int i = 0; i < F.n_seg; ++i) wt_ok = wt_ok && F.seg_units[i] % 4 == 0;
+  F.wt_from = wt_ok ? wt_tail_from(blocks, units * 4) : 0xffffffffu;
   int logl = 0;
   while ((8 << logl) < g) ++logl;
   hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, false, true, true), dim3((unsigned)blocks, 1),

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Variants of the FP8_BLOCK strip kernel (qz_block.hip) linked with the default build's other
-# objects: NAME:FLAGS args, e.g. nb4_nt:-DQZ_BLK_NB=4\ -DQZ_BLK_ST=2.  "base" rebuilds qz_quant.hip
+# objects: NAME:FLAGS args, e.g. nb4:-DQZ_BLK_NB=4.  "base" rebuilds qz_quant.hip
 # with QZ_BLK_FAST=0 (the round-1 k_tile_fast path) instead.  Output: build/tune/libqz_NAME.so
 set -e
 cd "$(dirname "$0")/../quantizers_amd/csrc"

@@ -688,9 +688,9 @@ def test_fp8_block_batch_and_zero_blocks(cuda):
 
 
 def test_fp8_block_store_policies_agree(cuda):
-    """The strip kernel writes its codes write-through (sc1) in launches moving < 768 MiB and
-    non-temporally above: a [9, 8192, 4096] batch (906 MB moved, nt stores) == its nine per-slice
-    launches (135 MB each, sc1 stores), and slice 4 == the plain-C oracle."""
+    """A large batch launch and small per-slice launches of the strip kernel agree (the store
+    policy was once chosen by launch size, qz_block.hip): a [9, 8192, 4096] batch (906 MB moved)
+    == its nine per-slice launches (135 MB each), and slice 4 == the plain-C oracle."""
     import qref
     a = QuantizationArgs(**FP8_BLOCK)
     g = torch.Generator(device=cuda).manual_seed(14)
