@@ -99,6 +99,8 @@ def _grid_scales_bf16(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], rati
         return s.float()
     out.copy_(s)
     return out
+
+
 PHASES: Dict[str, float] = {}  # phase name -> seconds, accumulated while PHASE_TIMING
 
 

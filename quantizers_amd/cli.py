@@ -27,6 +27,9 @@ from typing import Optional
 
 import torch
 
+# under torchrun only rank 0 holds the model's host image (load_model); True: one copy per rank
+RANK_COPIES = False
+
 
 def setup_logging(log_file: Optional[str] = None, level: int = logging.INFO):
     handlers = [logging.StreamHandler(sys.stdout)]
