@@ -207,3 +207,36 @@ def test_many_on_two_streams(cuda):
     for o, r in zip(outs, refs):  # read on the default stream right after (no synchronize)
         for k in ("codes", "scale", "global_scale"):
             _same(o[k], r[k])
+
+
+def test_plan_stacked_experts_take_two_stream_call(cuda, monkeypatch):
+    """a stacked NVFP4 unit (every expert of a fused Qwen3-MoE parameter) in
+    CompressionPlan.run goes through ops.quantize_nvfp4_many (the two-stream call), and its
+    on-disk tensors equal the per-expert quantize of each slice."""
+    from test_oneshot_gpu import _qwen3_moe
+    from quantizers_amd.compressor import CompressionPlan, compression_units
+    from quantizers_amd.model import iter_linears
+    from quantizers_amd.quantization import preset_scheme
+    m = _qwen3_moe().to(cuda)
+    nv = preset_scheme("NVFP4", ["Linear"])
+    m.quantization_scheme_map = {r.name: nv for r in iter_linears(m) if r.index is not None}
+    units, _ = compression_units(m)
+    plan = CompressionPlan(units, cuda)
+    stacked = [u for u in units if u.stacked]
+    assert len(stacked) == 6 and len(plan.singles) == 6  # 2 layers x (gate, up, down)
+    calls = []
+    real = ops.quantize_nvfp4_many
+
+    def spy(items, a, **kw):
+        calls.append(len(items))
+        return real(items, a, **kw)
+    monkeypatch.setattr(ops, "quantize_nvfp4_many", spy)
+    plan.run()
+    torch.cuda.synchronize()
+    assert sum(calls) == 6, calls
+    got = plan.tensors()
+    for u in stacked:
+        for g in u.refs:
+            want = ops.compress_weight(g.weight.contiguous(), nv.weights)
+            for k, v in want.items():
+                assert torch.equal(got[f"{g.name}.{k}"].cpu(), v.cpu()), (g.name, k)
