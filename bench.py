@@ -834,6 +834,24 @@ def main():
     if args.profile_only:
         return
 
+    # steady state of the same plan (informational, never `value`): the clocks settle about 25
+    # steps (35 ms) after the load starts (scripts/step_ramp.py, profiles/r05j_step_ramp.log), so
+    # a short K = 20 window after W = 5 includes part of that ramp
+    for _ in range(50):
+        plan.run(stream)
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s0.record(stream)
+    for _ in range(100):
+        plan.run(stream)
+    s1.record(stream)
+    torch.cuda.synchronize()
+    steady_ms = s0.elapsed_time(s1) / 100
+    steady = {"warmup_steps": 50, "steps": 100, "event_ms_per_step": steady_ms,
+              "params_per_s": params_step / (steady_ms * 1e-3),
+              "frac": alg_step / (steady_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+              "how": "HIP events around 100 steps after 50 more untimed ones, right after the timed region; "
+                     "informational (value and roofline use the W / K given)"}
+
     # per-launch durations of one extra (untimed) step, one event pair per launch
     per_launch = []
     for gq, part, *_ in plan.grouped:
@@ -972,6 +990,7 @@ def main():
                          "event_ms_per_step": ev_ms / args.steps,
                          "traffic_unit": "HBM bytes per launch (alg_bytes_per_launch beside it)"},
             "per_launch": per_launch,
+            "steady_state": steady,
             "cpu_baseline": cpu,
             "parity_check": ok,
             "ranks_seen": ranks_seen,

@@ -262,6 +262,29 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
                              size_t workspace_bytes, qz_stream_t stream);
 
 /*
+ * Segmented statistics (round 5) -- n <= 16 independent operands of one column count in ONE
+ * launch: segment s adds exactly what its own single call would (qz_awq_absmean_accum(x[s],
+ * tokens[s], channels, ld[s], sums[s], ...) / qz_awq_weight_mean_accum(w[s], rows[s], cols,
+ * ld[s], group_size, wsums[s], ...)), bit for bit: the same chunking and reduction tree per
+ * segment.  The output pointers must be distinct.  Returns QZ_ERR_FORMAT, launching nothing, when
+ * a segment would not take the single call's one-launch plan (unaligned or wide-ld operands,
+ * too many counters; the *_workspace_size functions then return 0): issue single calls instead.
+ * Replaces the per-sample calls of the AWQ activation hook over one batched calibration forward
+ * and the per-balance-layer calls of _compute_layer_means for one mapping.  The statistics
+ * workspace contract above applies.
+ */
+size_t qz_awq_absmean_segments_workspace_size(int32_t n, const int64_t* tokens, int64_t channels);
+int qz_awq_absmean_accum_segments(int32_t n, const void* const* x, const int64_t* tokens,
+                                  int64_t channels, const int64_t* ld, float* const* sums,
+                                  void* workspace, size_t workspace_bytes, qz_stream_t stream);
+size_t qz_awq_weight_mean_segments_workspace_size(int32_t n, const int64_t* rows, int64_t cols,
+                                                  int32_t group_size);
+int qz_awq_weight_mean_accum_segments(int32_t n, const void* const* w, const int64_t* rows,
+                                      int64_t cols, const int64_t* ld, int32_t group_size,
+                                      double* const* wsums, void* workspace,
+                                      size_t workspace_bytes, qz_stream_t stream);
+
+/*
  * qz_awq_stats_layout -- the reduction plan the statistics calls use for a [rows, cols] input
  * (which = 0: absmean, rows = tokens; 1: w_mean with group_size): out[0] one-launch (1) or
  * two-launch (0), out[1] column window, out[2] rows per chunk, out[3] chunks, out[4] row slots

@@ -27,7 +27,8 @@ EXPORTS = (
     "qz_strerror", "qz_version", "qz_build_config", "qz_quantize_workspace_size", "qz_quantize", "qz_quantize_qparams",
     "qz_observe_minmax", "qz_calculate_qparams", "qz_dequantize", "qz_pack_int32",
     "qz_awq_absmean_workspace_size", "qz_awq_absmean_accum", "qz_awq_weight_mean_workspace_size",
-    "qz_awq_weight_mean_accum",
+    "qz_awq_weight_mean_accum", "qz_awq_absmean_segments_workspace_size", "qz_awq_absmean_accum_segments",
+    "qz_awq_weight_mean_segments_workspace_size", "qz_awq_weight_mean_accum_segments",
     "qz_awq_grid_scales", "qz_awq_fake_quant", "qz_scale_columns", "qz_scale_rows",
     "qz_awq_grid_scales_batched", "qz_awq_fake_quant_batched", "qz_awq_sq_err_workspace_size",
     "qz_awq_sq_err_accum", "qz_quantize_many", "qz_quantize_grouped", "qz_quantize_grouped_var",
@@ -82,6 +83,10 @@ def load() -> ctypes.CDLL:
         "qz_awq_absmean_accum": ([P, I64, I64, I64, P, P, SZ, P], ctypes.c_int),
         "qz_awq_weight_mean_workspace_size": ([I64, I64, I32], SZ),
         "qz_awq_weight_mean_accum": ([P, I64, I64, I64, I32, P, P, SZ, P], ctypes.c_int),
+        "qz_awq_absmean_segments_workspace_size": ([I32, P, I64], SZ),
+        "qz_awq_absmean_accum_segments": ([I32, P, P, I64, P, P, P, SZ, P], ctypes.c_int),
+        "qz_awq_weight_mean_segments_workspace_size": ([I32, P, I64, I32], SZ),
+        "qz_awq_weight_mean_accum_segments": ([I32, P, P, I64, P, I32, P, P, SZ, P], ctypes.c_int),
         "qz_awq_stats_layout": ([I32, I64, I64, I32, P], ctypes.c_int),
         "qz_awq_grid_scales": ([P, P, I64, ctypes.c_float, I32, P, P], ctypes.c_int),
         "qz_awq_fake_quant": ([P, I64, I64, I64, I64, I64, A, P, P, P, SZ, P], ctypes.c_int),

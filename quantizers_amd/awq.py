@@ -354,12 +354,41 @@ class _AbsMean:
 
     def _hook(self, mod, args):
         j = _slot()
-        for x in _split_samples(args[0]):  # one add per calibration sample, as per-sample calls did
+        xs = _split_samples(args[0])
+        if j is None and len(xs) > 1:  # a batched calibration forward: every sample in one launch
+            self.add_samples(xs)
+            return
+        for x in xs:  # one add per calibration sample, as per-sample calls did
             if j is None:
                 self.add(x)
             elif x.numel():  # concurrent samples: this sample's total alone, added in order by finish()
                 part = torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device)
                 self.slots.setdefault(j, []).append((part, ops.awq_absmean_accum(x.detach(), part)))
+
+    def add_samples(self, xs: List[torch.Tensor]):
+        """``add(x)`` for every sample in order, as ONE segmented launch (ops.awq_absmean_segments):
+        each sample's total from zero, bit-identical to its own call, then combined as the
+        sequential adds combine them (f32 sum += total in sample order; bf16: one part each)."""
+        xs = [x.detach() if x.dtype == torch.bfloat16 else x.detach().to(torch.bfloat16) for x in xs]
+        live = [x for x in xs if x.numel()]
+        if not live:
+            for x in xs:
+                self.add(x)
+            return
+        parts = {id(x): torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device) for x in live}
+        counts = dict(zip((id(x) for x in live), ops.awq_absmean_segments(live, [parts[id(x)] for x in live])))
+        for x in xs:
+            if not x.numel():
+                self.add(x)
+                continue
+            part, n = parts[id(x)], counts[id(x)]
+            if self.bf16:
+                self.parts.append((part, n))
+            else:
+                if self.sum is None:
+                    self.sum = torch.zeros_like(part)
+                self.sum += part
+            self.count += n
 
     def finish(self):
         """sum = ((0 + t_0) + t_1) + ... over the samples in order: the kernel adds each call's
@@ -714,17 +743,34 @@ def _w_mean(groups: List[List[LinearRef]], quantized: Dict[str, QuantizationArgs
     if not bf16:
         wsum = torch.zeros(cols, dtype=torch.float64, device=device)
         rows = 0
-        for g in groups:
-            rows += ops.awq_weight_mean_accum(_view(g), _group_size_for_mean(quantized[g[0].name], cols), wsum)
+        for part, n in _w_mean_parts([(_view(g), _group_size_for_mean(quantized[g[0].name], cols)) for g in groups],
+                                     cols, device):
+            wsum += part  # ((0 + v_0) + v_1) + ...: the sequential calls' f64 adds
+            rows += n
         return (wsum / rows).float()
     acc, rows = None, 0
-    for ref in (refs if refs is not None else [x for g in groups for x in g]):
-        # every balance linear is a layer of its own (each expert slice too)
-        part = torch.zeros(cols, dtype=torch.float64, device=device)
-        rows += ops.awq_weight_mean_accum(ref.weight, _group_size_for_mean(quantized[ref.name], cols), part)
+    # every balance linear is a layer of its own (each expert slice too)
+    for part, n in _w_mean_parts([(ref.weight, _group_size_for_mean(quantized[ref.name], cols)) for ref in
+                                  (refs if refs is not None else [x for g in groups for x in g])], cols, device):
         sb = part.to(torch.bfloat16)
         acc = sb if acc is None else acc + sb
+        rows += n
     return acc / rows
+
+
+def _w_mean_parts(items: List[Tuple[torch.Tensor, int]], cols: int, device) -> List[Tuple[torch.Tensor, int]]:
+    """[(weight, group size)] -> [(its f64 column sums from zero, its rows)] in order: the weights
+    of one group size in segmented launches (ops.awq_weight_mean_segments: one launch per mapping
+    instead of one per balance layer, each sum bit-identical to its own call)."""
+    parts = [torch.zeros(cols, dtype=torch.float64, device=device) for _ in items]
+    rows = [0] * len(items)
+    by_g: Dict[int, List[int]] = {}
+    for i, (_, g) in enumerate(items):
+        by_g.setdefault(g, []).append(i)
+    for g, idx in by_g.items():
+        for i, n in zip(idx, ops.awq_weight_mean_segments([items[i][0] for i in idx], g, [parts[i] for i in idx])):
+            rows[i] = n
+    return list(zip(parts, rows))
 
 
 def _launch_groups(r: ResolvedMapping, quantized: Dict[str, QuantizationArgs]):

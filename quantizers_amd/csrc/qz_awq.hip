@@ -165,7 +165,7 @@ constexpr int QZ_ABS1_MIN_RC = 256; // minimum tokens per chunk
 constexpr int QZ_WM1_WIN = 128; // w_mean column window (at least the group size)
 constexpr int QZ_WM1_WPB = 8;
 constexpr int QZ_WM1_NB = 4;
-constexpr int QZ_WM1_BLOCKS = 256; // target workgroups of the one-launch w_mean
+constexpr int QZ_WM1_BLOCKS = 256; // target workgroups of the one-launch w_mean (power-of-two widths; wm1_blocks)
 constexpr int QZ_WM1_MIN_RC = 128; // minimum rows per chunk
 
 // rows rb + q, rb + q + S, ... < r1 of this lane's 8 columns (base = column pointer), SNB rows per
@@ -260,7 +260,7 @@ __device__ __forceinline__ T reduce_rows(T (*red)[WIN], const T* src, int64_t n,
 
 template <int WIN, int SWP, typename T>
 __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int lane, int wv, int64_t C, int64_t nch,
-                                             int64_t cpg, T* part, T* gpart, unsigned* cnt, T* sum, T pre) {
+                                             int64_t cpg, T* part, T* gpart, unsigned* cnt, T* sum, T pre, int64_t k) {
   constexpr int LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, NT = SWP * 64, TF = NT / WIN;
   static_assert(TF >= 1 && NT % WIN == 0 && S >= TF, "stats window");
   const int q = lane / LPR, c8 = lane % LPR;
@@ -268,7 +268,6 @@ __device__ __forceinline__ void stats_finish(T (*red)[WIN], const T* acc, int la
   for (int i = 0; i < 8; ++i) red[wv * RPW + q][c8 * 8 + i] = acc[i];
   __syncthreads();
   const int64_t cb = (int64_t)blockIdx.x * WIN;
-  const int64_t k = blockIdx.y;
   for (int j = threadIdx.x; j < WIN; j += NT) {
     const int64_t c = cb + j;
     if (c < C) {
@@ -303,16 +302,16 @@ __device__ __forceinline__ T stats_pre(const T* sum, int64_t C) {
   return (threadIdx.x < WIN && c < C) ? sum[c] : T(0);
 }
 
+// chunk k of one [T, C] operand (the whole launch, or one segment of a segmented launch)
 template <int WIN>
-__global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
-                                                                int64_t tc, int64_t nch, int64_t cpg, float* part,
-                                                                float* gpart, unsigned* cnt, float* sum) {
+__device__ __forceinline__ void absmean_chunk(float (*red)[WIN], const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                              int64_t tc, int64_t nch, int64_t cpg, float* part, float* gpart,
+                                              unsigned* cnt, float* sum, int64_t k) {
   constexpr int SWP = QZ_ABS1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW;
-  __shared__ float red[S][WIN];
   // wave index through readfirstlane: known wave-uniform, so row bases stay in SGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
-  const int64_t t0 = (int64_t)blockIdx.y * tc, t1 = std::min<int64_t>(T, t0 + tc);
+  const int64_t t0 = k * tc, t1 = std::min<int64_t>(T, t0 + tc);
   const float pre = stats_pre<WIN>(sum, C);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   auto row = [&](const uint4 v, bool ok) {
@@ -324,7 +323,44 @@ __global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t*
     }
   };
   stats_walk<S, QZ_ABS1_NB>(x + c0, ld, t0 + wv * RPW, q, t1, row);
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum, pre);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, sum, pre, k);
+}
+
+template <int WIN>
+__global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_1l(const uint16_t* x, int64_t T, int64_t C, int64_t ld,
+                                                                int64_t tc, int64_t nch, int64_t cpg, float* part,
+                                                                float* gpart, unsigned* cnt, float* sum) {
+  __shared__ float red[QZ_ABS1_WPB * 64 / (WIN / 8)][WIN];
+  absmean_chunk<WIN>(red, x, T, C, ld, tc, nch, cpg, part, gpart, cnt, sum, blockIdx.y);
+}
+
+// Segmented statistics (round 5): n independent operands of one column count in ONE launch --
+// the calibration samples of one batched forward (absmean), the balance layers of one mapping
+// (w_mean).  Segment s keeps exactly the chunking, workgroup order and reduction tree of its own
+// single call (its chunks are grid rows chunk0[s] .. chunk0[s + 1] - 1, its partials, group
+// partials and arrival counters their own slices of the workspace), so every out[s] is
+// bit-identical to that call's result.
+constexpr int QZ_STATS_SEGS = 16;
+struct StatsSegs {
+  const uint16_t* x[QZ_STATS_SEGS];
+  void* out[QZ_STATS_SEGS];
+  int64_t rows[QZ_STATS_SEGS], ld[QZ_STATS_SEGS], rc[QZ_STATS_SEGS], nch[QZ_STATS_SEGS];
+  int64_t chunk0[QZ_STATS_SEGS + 1], gchunk0[QZ_STATS_SEGS], cnt0[QZ_STATS_SEGS];
+  int32_t n;
+};
+__device__ __forceinline__ int seg_of(const StatsSegs& S, int64_t y) {  // wave-uniform
+  int s = 0;
+  while (s + 1 < S.n && y >= S.chunk0[s + 1]) ++s;
+  return s;
+}
+
+template <int WIN>
+__global__ __launch_bounds__(QZ_ABS1_WPB * 64) void k_absmean_seg(StatsSegs S, int64_t C, int64_t cpg, float* part,
+                                                                 float* gpart, unsigned* cnt) {
+  __shared__ float red[QZ_ABS1_WPB * 64 / (WIN / 8)][WIN];
+  const int s = seg_of(S, blockIdx.y);
+  absmean_chunk<WIN>(red, S.x[s], S.rows[s], C, S.ld[s], S.rc[s], S.nch[s], cpg, part + S.chunk0[s] * C,
+                     gpart + S.gchunk0[s] * C, cnt + S.cnt0[s], (float*)S.out[s], blockIdx.y - S.chunk0[s]);
 }
 
 typedef float qz_f32x2 __attribute__((ext_vector_type(2)));
@@ -336,16 +372,15 @@ __device__ __forceinline__ float bfr1(float v) {
 }
 
 template <int WIN, int LOGL>
-__global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w, int64_t R, int64_t C, int64_t ld,
-                                                             int64_t rc, int64_t nch, int64_t cpg, double* part,
-                                                             double* gpart, unsigned* cnt, double* wsum) {
+__device__ __forceinline__ void wmean_chunk(double (*red)[WIN], const uint16_t* w, int64_t R, int64_t C, int64_t ld,
+                                            int64_t rc, int64_t nch, int64_t cpg, double* part, double* gpart,
+                                            unsigned* cnt, double* wsum, int64_t k) {
   constexpr int SWP = QZ_WM1_WPB, LPR = WIN / 8, RPW = 64 / LPR, S = SWP * RPW, L = 1 << LOGL;
   static_assert(L <= LPR, "a group must lie inside one row segment of the window");
-  __shared__ double red[S][WIN];
   // wave index through readfirstlane: known wave-uniform, so row bases stay in SGPRs
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = lane / LPR;
   const int64_t c0 = std::min<int64_t>((int64_t)blockIdx.x * WIN + (lane % LPR) * 8, C - 8);
-  const int64_t r0 = (int64_t)blockIdx.y * rc, r1 = std::min<int64_t>(R, r0 + rc);
+  const int64_t r0 = k * rc, r1 = std::min<int64_t>(R, r0 + rc);
   const double pre = stats_pre<WIN>(wsum, C);
   double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto row = [&](const uint4 v, bool ok) {
@@ -362,7 +397,24 @@ __global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w,
     }
   };
   stats_walk<S, QZ_WM1_NB>(w + c0, ld, r0 + wv * RPW, q, r1, row);
-  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum, pre);
+  stats_finish<WIN, SWP>(red, acc, lane, wv, C, nch, cpg, part, gpart, cnt, wsum, pre, k);
+}
+
+template <int WIN, int LOGL>
+__global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_1l(const uint16_t* w, int64_t R, int64_t C, int64_t ld,
+                                                             int64_t rc, int64_t nch, int64_t cpg, double* part,
+                                                             double* gpart, unsigned* cnt, double* wsum) {
+  __shared__ double red[QZ_WM1_WPB * 64 / (WIN / 8)][WIN];
+  wmean_chunk<WIN, LOGL>(red, w, R, C, ld, rc, nch, cpg, part, gpart, cnt, wsum, blockIdx.y);
+}
+
+template <int WIN, int LOGL>
+__global__ __launch_bounds__(QZ_WM1_WPB * 64) void k_wmean_seg(StatsSegs S, int64_t C, int64_t cpg, double* part,
+                                                              double* gpart, unsigned* cnt) {
+  __shared__ double red[QZ_WM1_WPB * 64 / (WIN / 8)][WIN];
+  const int s = seg_of(S, blockIdx.y);
+  wmean_chunk<WIN, LOGL>(red, S.x[s], S.rows[s], C, S.ld[s], S.rc[s], S.nch[s], cpg, part + S.chunk0[s] * C,
+                         gpart + S.gchunk0[s] * C, cnt + S.cnt0[s], (double*)S.out[s], blockIdx.y - S.chunk0[s]);
 }
 
 // chunking of the one-launch kernels: >= min_rc rows per chunk, about `blocks` workgroups
@@ -779,11 +831,20 @@ int qz_awq_sq_err_reduce(const double* part, int64_t n, int64_t nb, int64_t part
   return launch_err();
 }
 
+// target workgroups of a one-launch w_mean: 256 when the row pitch is a power of two, else 512
+// (1024 from 96 MB).  profiles/r05i-k_tune_stats*: at 256 workgroups rows of 2560 / 3072 columns
+// stream at 3.3-3.9 TB/s against 5-5.8 TB/s for 2048 / 4096; more row chunks recover most of it
+// ([19456, 2560]: 29.8 -> 23.9 us; [9728, 2560]: 17.1 -> 15.2 us; [24576, 3072]: 41.4 -> 34.4
+// us) while power-of-two widths lose with them ([11008, 4096]: 18.0 -> 20.4 us)
+static int64_t wm1_blocks(int64_t rows, int64_t cols) {
+  if ((cols & (cols - 1)) == 0) return QZ_WM1_BLOCKS;
+  return rows * cols * 2 >= (96ll << 20) ? 4 * QZ_WM1_BLOCKS : 2 * QZ_WM1_BLOCKS;
+}
 // one-launch plan of a w_mean call (chunks), or -1 (two-launch / generic paths)
 static int64_t wmean_1l(int64_t rows, int64_t cols, int64_t g, int64_t* rc) {
   if (g < 8 || g > 512 || (g & (g - 1))) return -1;
   const int win = wmean_win(g);
-  const int64_t n1 = stats1_chunks(rows, cols, win, QZ_WM1_BLOCKS, QZ_WM1_MIN_RC, rc);
+  const int64_t n1 = stats1_chunks(rows, cols, win, wm1_blocks(rows, cols), QZ_WM1_MIN_RC, rc);
   return stats1_counters_fit(cols, win, n1) ? n1 : -1;
 }
 
@@ -867,6 +928,136 @@ int qz_awq_weight_mean_accum(const void* w, int64_t rows, int64_t cols, int64_t 
     hipLaunchKernelGGL(k_wmean_generic, dim3((unsigned)cdiv(cols, 256)), dim3(256), 0, st, (const uint16_t*)w, rows,
                        cols, ld, g, wsum);
   }
+  return launch_err();
+}
+
+// the segment table of a segmented call: every segment on its single call's one-launch plan;
+// false when one is not (the caller then issues single calls)
+static bool segs_plan(int which, int32_t n, const int64_t* rows, int64_t cols, int32_t g, StatsSegs* S,
+                      int64_t* ws_bytes) {
+  if (n < 1 || n > QZ_STATS_SEGS || cols <= 0 || !rows) return false;
+  const int win = which == 0 ? ABS1_WIN : wmean_win(g);
+  const int64_t bx = cdiv(cols, win), elem = which == 0 ? 4 : 8;
+  int64_t chunks = 0, groups = 0, cnts = 0;
+  S->n = n;
+  for (int s = 0; s < n; ++s) {
+    if (rows[s] <= 0 || rows[s] >= INT32_MAX) return false;
+    int64_t rc = 0;
+    const int64_t n1 = which == 0 ? absmean_1l(rows[s], cols, &rc) : wmean_1l(rows[s], cols, g, &rc);
+    if (n1 <= 0) return false;
+    const int64_t ng = cdiv(n1, QZ_STATS_CPG);
+    S->rows[s] = rows[s];
+    S->rc[s] = rc;
+    S->nch[s] = n1;
+    S->chunk0[s] = chunks;
+    S->gchunk0[s] = groups;
+    S->cnt0[s] = cnts;
+    chunks += n1;
+    groups += ng;
+    cnts += bx * (ng + 1);
+  }
+  S->chunk0[n] = chunks;
+  if (cnts > STATS_CNT || chunks > 65535) return false;
+  *ws_bytes = STATS_HEAD + elem * (chunks + groups) * cols;
+  return true;
+}
+
+static bool segs_inputs_ok(int32_t n, const void* const* x, const int64_t* ld, int64_t cols, void* const* out,
+                           size_t out_align) {
+  if (cols % 8) return false;
+  for (int s = 0; s < n; ++s) {
+    if (!x[s] || !out[s] || !aligned(x[s], 16) || !aligned(out[s], out_align) || ld[s] < cols || ld[s] % 8 ||
+        ld[s] >= INT32_MAX)
+      return false;
+    for (int t = 0; t < s; ++t)
+      if (out[t] == out[s]) return false;  // each segment its own sums (no two reducers on one row)
+  }
+  return true;
+}
+
+size_t qz_awq_absmean_segments_workspace_size(int32_t n, const int64_t* tokens, int64_t channels) {
+  StatsSegs S;
+  int64_t b = 0;
+  return segs_plan(0, n, tokens, channels, 0, &S, &b) ? (size_t)b : 0;
+}
+
+int qz_awq_absmean_accum_segments(int32_t n, const void* const* x, const int64_t* tokens, int64_t channels,
+                                  const int64_t* ld, float* const* sums, void* workspace, size_t workspace_bytes,
+                                  qz_stream_t stream) {
+  if (!x || !tokens || !ld || !sums) return QZ_ERR_NULL;
+  StatsSegs S;
+  int64_t need = 0;
+  if (!segs_plan(0, n, tokens, channels, 0, &S, &need) ||
+      !segs_inputs_ok(n, x, ld, channels, (void* const*)sums, 4))
+    return QZ_ERR_FORMAT;
+  if (!workspace || (int64_t)workspace_bytes < need) return QZ_ERR_WORKSPACE;
+  if (!aligned(workspace, 16)) return QZ_ERR_ALIGN;
+  for (int s = 0; s < n; ++s) {
+    S.x[s] = (const uint16_t*)x[s];
+    S.ld[s] = ld[s];
+    S.out[s] = sums[s];
+  }
+  float* p1 = (float*)((char*)workspace + STATS_HEAD);
+  hipLaunchKernelGGL(k_absmean_seg<ABS1_WIN>, dim3((unsigned)cdiv(channels, ABS1_WIN), (unsigned)S.chunk0[n]),
+                     dim3(QZ_ABS1_WPB * 64), 0, (hipStream_t)stream, S, channels, (int64_t)QZ_STATS_CPG, p1,
+                     p1 + S.chunk0[n] * channels, (unsigned*)workspace);
+  return launch_err();
+}
+
+size_t qz_awq_weight_mean_segments_workspace_size(int32_t n, const int64_t* rows, int64_t cols, int32_t group_size) {
+  StatsSegs S;
+  int64_t b = 0;
+  return segs_plan(1, n, rows, cols, group_size, &S, &b) ? (size_t)b : 0;
+}
+
+extern "C++" {
+template <int WIN>
+static void launch_wmean_seg(int logl, dim3 grid, dim3 blk, hipStream_t st, const StatsSegs& S, int64_t cols,
+                             double* p1, double* gp, unsigned* cnt) {
+  const int64_t cpg = QZ_STATS_CPG;
+  switch (logl) {
+    case 0: hipLaunchKernelGGL((k_wmean_seg<WIN, 0>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt); break;
+    case 1: hipLaunchKernelGGL((k_wmean_seg<WIN, 1>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt); break;
+    case 2: hipLaunchKernelGGL((k_wmean_seg<WIN, 2>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt); break;
+    case 3: hipLaunchKernelGGL((k_wmean_seg<WIN, 3>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt); break;
+    case 4: hipLaunchKernelGGL((k_wmean_seg<WIN, 4>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt); break;
+    case 5:
+      if constexpr (WIN >= 256) hipLaunchKernelGGL((k_wmean_seg<WIN, 5>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt);
+      break;
+    default:
+      if constexpr (WIN >= 512) hipLaunchKernelGGL((k_wmean_seg<WIN, 6>), grid, blk, 0, st, S, cols, cpg, p1, gp, cnt);
+      break;
+  }
+}
+}  // extern "C++"
+
+int qz_awq_weight_mean_accum_segments(int32_t n, const void* const* w, const int64_t* rows, int64_t cols,
+                                      const int64_t* ld, int32_t group_size, double* const* wsums, void* workspace,
+                                      size_t workspace_bytes, qz_stream_t stream) {
+  if (!w || !rows || !ld || !wsums) return QZ_ERR_NULL;
+  if (group_size <= 0 || cols % group_size) return QZ_ERR_GROUP;
+  StatsSegs S;
+  int64_t need = 0;
+  if (!segs_plan(1, n, rows, cols, group_size, &S, &need) ||
+      !segs_inputs_ok(n, w, ld, cols, (void* const*)wsums, 8))
+    return QZ_ERR_FORMAT;
+  if (!workspace || (int64_t)workspace_bytes < need) return QZ_ERR_WORKSPACE;
+  if (!aligned(workspace, 8)) return QZ_ERR_ALIGN;
+  for (int s = 0; s < n; ++s) {
+    S.x[s] = (const uint16_t*)w[s];
+    S.ld[s] = ld[s];
+    S.out[s] = wsums[s];
+  }
+  int logl = 0;
+  while ((8 << logl) < group_size) ++logl;
+  const int win = wmean_win(group_size);
+  const dim3 grid((unsigned)cdiv(cols, win), (unsigned)S.chunk0[n]), blk(QZ_WM1_WPB * 64);
+  double* p1 = (double*)((char*)workspace + STATS_HEAD);
+  double* gp = p1 + S.chunk0[n] * cols;
+  hipStream_t st = (hipStream_t)stream;
+  if (win == 512) launch_wmean_seg<512>(logl, grid, blk, st, S, cols, p1, gp, (unsigned*)workspace);
+  else if (win == 256) launch_wmean_seg<256>(logl, grid, blk, st, S, cols, p1, gp, (unsigned*)workspace);
+  else launch_wmean_seg<128>(logl, grid, blk, st, S, cols, p1, gp, (unsigned*)workspace);
   return launch_err();
 }
 

@@ -1511,7 +1511,7 @@ int nv_launch(NvArgs& A, bool tab, void* sync, size_t sync_bytes, hipStream_t st
   rc = launch_err();
   // the |w| max launch has run but the encode (which resets the sync lines) has not: clear them,
   // so the region is zero for the next call on this stream as the contract says
-  if (rc) hipMemsetAsync(A.sync, 0, 4 * NV_SYNC_STRIDE * (size_t)A.n_slices, st);
+  if (rc) (void)hipMemsetAsync(A.sync, 0, 4 * NV_SYNC_STRIDE * (size_t)A.n_slices, st);
   return rc;
 }
 

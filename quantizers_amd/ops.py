@@ -669,6 +669,71 @@ def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) 
     return r
 
 
+STATS_SEGS = 16  # segments per segmented statistics launch (QZ_STATS_SEGS)
+
+
+def _rows2d(t: torch.Tensor) -> torch.Tensor:
+    t2 = t.reshape(-1, t.shape[-1])
+    return t2 if t2.stride(-1) == 1 else t2.contiguous()
+
+
+def _segments(fn_ws, fn_run, single, ts: List[torch.Tensor], outs: List[torch.Tensor], *extra) -> List[int]:
+    """Issue ts[i] -> outs[i] as segmented launches of <= STATS_SEGS operands; a batch the C side
+    declines (QZ_ERR_FORMAT: a segment off its single call's one-launch plan) runs as single calls,
+    which give the same bits."""
+    lib = _lib.load()
+    counts = []
+    for i0 in range(0, len(ts), STATS_SEGS):
+        t2 = [_rows2d(t) for t in ts[i0:i0 + STATS_SEGS]]
+        o = outs[i0:i0 + STATS_SEGS]
+        n, cols = len(t2), t2[0].shape[1]
+        rows = (ctypes.c_int64 * n)(*[t.shape[0] for t in t2])
+        lds = (ctypes.c_int64 * n)(*[t.stride(0) for t in t2])
+        ptrs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in t2])
+        optrs = (ctypes.c_void_p * n)(*[x.data_ptr() for x in o])
+        need = getattr(lib, fn_ws)(n, rows, cols, *extra)
+        rc = _lib.QZ_ERR_FORMAT
+        if need:
+            ws = stats_workspace(need + 256, t2[0].device)
+            rc = getattr(lib, fn_run)(n, ptrs, rows, cols, lds, *extra, optrs, _ptr(ws), ws.numel(), _stream())
+        if rc == _lib.QZ_ERR_FORMAT:
+            for t, x in zip(t2, o):
+                single(t, x)
+        else:
+            _lib.check(rc, fn_run)
+        counts += [t.shape[0] for t in t2]
+    return counts
+
+
+def awq_absmean_segments(xs: List[torch.Tensor], sums: List[torch.Tensor]) -> List[int]:
+    """sums[i][c] += sum_t |xs[i][t, c]| for every i in ONE launch (qz_awq_absmean_accum_segments),
+    bit-identical to awq_absmean_accum(xs[i], sums[i]) each; the sums must be distinct tensors and
+    the operands non-empty bf16 device tensors of one channel count.  Returns the token counts."""
+    if not xs:
+        return []
+    for x, o in zip(xs, sums):
+        _check_dev(x, "activations")
+        if x.dtype != torch.bfloat16 or x.numel() == 0 or o.dtype != torch.float32 or x.shape[-1] != xs[0].shape[-1]:
+            raise ValueError("awq_absmean_segments: non-empty bf16 operands of one width, float32 sums")
+    return _segments("qz_awq_absmean_segments_workspace_size", "qz_awq_absmean_accum_segments",
+                     awq_absmean_accum, xs, sums)
+
+
+def awq_weight_mean_segments(ws: List[torch.Tensor], group_size: int, wsums: List[torch.Tensor]) -> List[int]:
+    """wsums[i][c] += w_mean column sums of ws[i] for every i in ONE launch
+    (qz_awq_weight_mean_accum_segments), bit-identical to awq_weight_mean_accum(ws[i], group_size,
+    wsums[i]) each; distinct float64 sums, one column count.  Returns the row counts."""
+    if not ws:
+        return []
+    for w, o in zip(ws, wsums):
+        _check_dev(w, "weight")
+        if w.dtype != torch.bfloat16 or w.numel() == 0 or o.dtype != torch.float64 or w.shape[-1] != ws[0].shape[-1]:
+            raise ValueError("awq_weight_mean_segments: non-empty bf16 weights of one width, float64 sums")
+    g = int(group_size)
+    return _segments("qz_awq_weight_mean_segments_workspace_size", "qz_awq_weight_mean_accum_segments",
+                     lambda w, o: awq_weight_mean_accum(w, g, o), ws, wsums, g)
+
+
 def awq_sq_err_accum(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
     """out[0] += sum(f32(bf16(a - b))^2) (f64, deterministic): the AWQ grid loss numerator
     over two bf16 parent outputs of the same shape (qz_awq_sq_err_accum)."""

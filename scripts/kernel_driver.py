@@ -84,6 +84,24 @@ def main(n=30):
         ("fp8_block_grouped_q", lambda i: g_q.run(), 1),
         ("fp8_block_stack_kv", lambda i: ops.quantize_weight(stk, fb, out=stk_out), 1),
     ]
+    # the AWQ statistics in the pass's own pattern (Qwen3-4B: hidden 2560, 16 calibration samples of
+    # 2048 tokens per batched forward): absmean per sample as the hook issued it through round 4 and
+    # all 16 samples as one segmented launch (round 5); w_mean per balance layer ([9728, 2560]) and
+    # per mapping as one segmented launch (gate + up; q / k / v)
+    xl = [torch.randn(16 * 2048, 2560, device=dev, generator=gen).to(torch.bfloat16) for _ in range(2)]
+    smp = [[x[j * 2048:(j + 1) * 2048] for j in range(16)] for x in xl]
+    sums_l = [torch.zeros(2560, dtype=torch.float32, device=dev) for _ in range(16)]
+    gu_map = [[(torch.randn(9728, 2560, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for _ in range(2)]
+              for _ in range(3)]
+    qkv = [(torch.randn(r, 2560, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for r in (4096, 1024, 1024)]
+    wsum_l = [torch.zeros(2560, dtype=torch.float64, device=dev) for _ in range(3)]
+    kernels += [
+        ("absmean_sample_2048x2560", lambda i: ops.awq_absmean_accum(smp[i % 2][i % 16], sums_l[0]), 1),
+        ("absmean_seg_16x2048x2560", lambda i: ops.awq_absmean_segments(smp[i % 2], sums_l), 1),
+        ("wmean_balance_9728x2560", lambda i: ops.awq_weight_mean_accum(gu_map[i % 3][i % 2], G, wsum_l[0]), 1),
+        ("wmean_seg_gate_up", lambda i: ops.awq_weight_mean_segments(gu_map[i % 3], G, wsum_l[:2]), 1),
+        ("wmean_seg_q_k_v", lambda i: ops.awq_weight_mean_segments(qkv, G, wsum_l), 1),
+    ]
     st = torch.cuda.current_stream()
     for name, fn, _ in kernels:
         for i in range(3):

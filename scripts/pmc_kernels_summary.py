@@ -35,8 +35,22 @@ KERNELS = {
     "k_wmean_v8": ("AWQ w_mean stage 1", P * 2),
     "k_colsum_final<double>": ("AWQ w_mean stage 2", None),
     "k_scale_v8<true>": ("AWQ smoothing W[:, c] *= s[c]", P * 4 + C * 4),
-    "k_absmean_1l<": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
-    "k_wmean_1l<": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
+    # kernel_driver's absmean / w_mean legs in order: "#0" the [16384, 4096] / [11008, 4096]
+    # operands, "#1" the AWQ pass's own Qwen3-4B pattern as issued through round 4 (one calibration
+    # sample [2048, 2560]; one balance layer [9728, 2560]); the segmented launches of round 5 (16
+    # samples; gate + up, then q / k / v)
+    "k_absmean_1l<128>#0": ("AWQ absmean [16384, 4096], one launch (round 3)", T * C * 2),
+    "k_absmean_1l<128>#1": ("AWQ absmean, one calibration sample [2048, 2560] per launch (Qwen3-4B pass through r04)",
+                            2048 * 2560 * 2),
+    "k_absmean_seg<128>": ("AWQ absmean, 16 samples x [2048, 2560] in one segmented launch (round 5)",
+                           16 * 2048 * 2560 * 2),
+    "k_wmean_1l<128, 4>#0": ("AWQ w_mean [11008, 4096] g128, one launch (round 3)", P * 2),
+    "k_wmean_1l<128, 4>#1": ("AWQ w_mean, one balance layer [9728, 2560] per launch (Qwen3-4B pass through r04)",
+                             9728 * 2560 * 2),
+    "k_wmean_seg<128, 4>#0": ("AWQ w_mean, gate + up 2 x [9728, 2560] in one segmented launch (round 5)",
+                              2 * 9728 * 2560 * 2),
+    "k_wmean_seg<128, 4>#1": ("AWQ w_mean, q / k / v [4096 | 1024 | 1024, 2560] in one segmented launch (round 5)",
+                              6144 * 2560 * 2),
     # MXFP4 [128, 768, 2048] (BASELINE configs[3]): read 2 B + codes 0.5 B + e8m0 scale 1/32 B per param
     "k_group_fast<2, 2, false, true, true, false>": ("MXFP4 Qwen3-30B-A3B expert half [128, 768, 2048] (one launch)",
                                                      int(128 * 768 * 2048 * (2 + 0.5 + 1 / 32))),

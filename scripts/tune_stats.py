@@ -6,12 +6,15 @@ the Infinity Cache together), HIP events / 100 -> us per call (both stages).  Ro
 the builds; the median over rounds is printed.  Every build's sums are checked against the first
 build's: bit-equal when the reduction tree is the same, else to rtol 1e-5 (f32) / 1e-12 (f64)."""
 import ctypes
+import os
 import sys
 
 import torch
 
-T, C = 16384, 4096
-R, G = 11008, 128
+# operand shapes: ABS=TxC (absmean activations), WM=RxC (w_mean weight); defaults: the round-3 pair
+T, C = (int(v) for v in os.environ.get("ABS", "16384x4096").split("x"))
+R, WC = (int(v) for v in os.environ.get("WM", "11008x4096").split("x"))
+G = 128
 P = ctypes.c_void_p
 I64 = ctypes.c_int64
 
@@ -30,17 +33,17 @@ def bind(path):
 def main():
     dev = torch.device("cuda:0")
     xs = [torch.randn(T, C, device=dev).to(torch.bfloat16) for _ in range(4)]
-    ws = [(torch.randn(R, C, device=dev) * 0.02).to(torch.bfloat16) for _ in range(12)]
+    ws = [(torch.randn(R, WC, device=dev) * 0.02).to(torch.bfloat16) for _ in range(12)]
     st = torch.cuda.current_stream().cuda_stream
     builds = []
     for path in sys.argv[1:]:
         lib = bind(path)
         na = lib.qz_awq_absmean_workspace_size(T, C)
-        nw = lib.qz_awq_weight_mean_workspace_size(R, C, G)
+        nw = lib.qz_awq_weight_mean_workspace_size(R, WC, G)
         b = {"name": path.split("/")[-1], "lib": lib, "wa": torch.zeros(na, dtype=torch.uint8, device=dev),
              "ww": torch.zeros(nw, dtype=torch.uint8, device=dev),
              "sa": torch.zeros(C, dtype=torch.float32, device=dev),
-             "sw": torch.zeros(C, dtype=torch.float64, device=dev), "ta": [], "tw": []}
+             "sw": torch.zeros(WC, dtype=torch.float64, device=dev), "ta": [], "tw": []}
 
         def absmean(i, b=b):
             rc = b["lib"].qz_awq_absmean_accum(xs[i % 4].data_ptr(), T, C, C, b["sa"].data_ptr(), b["wa"].data_ptr(),
@@ -48,7 +51,7 @@ def main():
             assert rc == 0, rc
 
         def wmean(i, b=b):
-            rc = b["lib"].qz_awq_weight_mean_accum(ws[i % 12].data_ptr(), R, C, C, G, b["sw"].data_ptr(),
+            rc = b["lib"].qz_awq_weight_mean_accum(ws[i % 12].data_ptr(), R, WC, WC, G, b["sw"].data_ptr(),
                                                    b["ww"].data_ptr(), b["ww"].numel(), st)
             assert rc == 0, rc
         b["absmean"], b["wmean"] = absmean, wmean
@@ -80,7 +83,7 @@ def main():
         ta, tw = sorted(b["ta"]), sorted(b["tw"])
         ma, mw = ta[len(ta) // 2], tw[len(tw) // 2]
         print(f"{b['name']:28s} absmean {ma:7.2f} us ({T * C * 2 / ma / 1e3:6.0f} GB/s)  "
-              f"w_mean {mw:7.2f} us ({R * C * 2 / mw / 1e3:6.0f} GB/s)  "
+              f"w_mean {mw:7.2f} us ({R * WC * 2 / mw / 1e3:6.0f} GB/s)  "
               f"bit-equal (a, w)={b['eq']} close={b['close']}  ws={b['wa'].numel() / 1e6:.2f}/{b['ww'].numel() / 1e6:.2f} MB",
               flush=True)
 

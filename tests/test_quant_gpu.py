@@ -392,6 +392,49 @@ def test_weight_mean_deterministic_fixed_order(cuda, shape, g):
         assert torch.equal(o, want), (o - want).abs().max()
 
 
+def test_stats_segments_bit_identical_to_single_calls(cuda):
+    """Segmented statistics (one launch over many operands) == one single call per operand, bit
+    for bit: absmean over 17 calibration samples of a batched forward (two launches of <= 16
+    segments; ragged, strided and 1-token samples) into zero sums and into sums holding an earlier
+    total; w_mean over a Qwen3-4B mapping's balance layers (q / k / v, gate / up: the 2560-column
+    plans) at group 128 and 32, and over an unaligned operand (the whole batch then runs as single
+    calls).  The arrival counters are zero afterwards."""
+    g = torch.Generator(device=cuda).manual_seed(21)
+    base = torch.randn(17 * 2048 + 301, 3072, device=cuda, generator=g).to(torch.bfloat16)
+    xs = [base[i * 2048:(i + 1) * 2048, :2560] for i in range(16)] + [base[16 * 2048:16 * 2048 + 300, :2560]]
+    xs[3] = base[-1:, :2560]
+    for pre in (0.0, 3.5):
+        seg = [torch.full((2560,), pre, dtype=torch.float32, device=cuda) for _ in xs]
+        one = [t.clone() for t in seg]
+        assert ops.awq_absmean_segments(xs, seg) == [x.shape[0] for x in xs]
+        for x, o in zip(xs, one):
+            ops.awq_absmean_accum(x, o)
+        for a, b in zip(seg, one):
+            assert torch.equal(a, b)
+    ws = [(torch.randn(r, 2560, device=cuda, generator=g) * 0.02).to(torch.bfloat16) for r in (4096, 1024, 1024)]
+    ws += [(torch.randn(9728, 2560, device=cuda, generator=g) * 0.02).to(torch.bfloat16) for _ in range(2)]
+    for gs in (128, 32):
+        seg = [torch.zeros(2560, dtype=torch.float64, device=cuda) for _ in ws]
+        one = [t.clone() for t in seg]
+        assert ops.awq_weight_mean_segments(ws, gs, seg) == [w.shape[0] for w in ws]
+        for w, o in zip(ws, one):
+            ops.awq_weight_mean_accum(w, gs, o)
+        for a, b in zip(seg, one):
+            assert torch.equal(a, b)
+    odd = torch.empty(300 * 2568 + 8, dtype=torch.bfloat16, device=cuda)[1:1 + 300 * 2568].view(300, 2568)[:, :2560]
+    odd.copy_(ws[0][:300])
+    seg = [torch.zeros(2560, dtype=torch.float64, device=cuda) for _ in range(2)]
+    one = [t.clone() for t in seg]
+    ops.awq_weight_mean_segments([ws[1], odd], 128, seg)
+    ops.awq_weight_mean_accum(ws[1], 128, one[0])
+    ops.awq_weight_mean_accum(odd, 128, one[1])
+    for a, b in zip(seg, one):
+        assert torch.equal(a, b)
+    torch.cuda.synchronize()
+    for buf in ops._stats_ws_cache.values():
+        assert not buf[:32768].any()
+
+
 def test_smoothing_ops(cuda):
     w = _w(64, 128, seed=2)
     s = torch.rand(128, generator=torch.Generator().manual_seed(1)) + 0.5
