@@ -852,17 +852,20 @@ def main():
               "how": "HIP events around 100 steps after 50 more untimed ones, right after the timed region; "
                      "informational (value and roofline use the W / K given)"}
 
-    # per-launch durations of one extra (untimed) step, one event pair per launch
+    # per-launch durations (untimed, after the regions above): each launch 5 times back to back,
+    # one event pair per launch, the median (a single launch after a synchronize can catch a clock
+    # transient)
     per_launch = []
     for gq, part, *_ in plan.grouped:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        gq.run(stream)
-        e1.record(stream)
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        evs[0].record(stream)
+        for i in range(5):
+            gq.run(stream)
+            evs[i + 1].record(stream)
         torch.cuda.synchronize()
         nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
                                                          for t in o.values() if t is not None)
-        us = e0.elapsed_time(e1) * 1e3
+        us = sorted(evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(5))[2]
         rb = sum(w.numel() * 2 for _, w in part)
         per_launch.append({"shapes": sorted({f"{r}x{c}" for r, c in gq.shapes}), "weights": gq.n,
                            "us": us, "alg_bytes": nb, "read_bytes": rb,
