@@ -82,6 +82,37 @@ def _running_mean_bf16(parts) -> Optional[torch.Tensor]:
     return m
 
 
+def _running_means_bf16(parts: torch.Tensor, counts: List[List[int]]) -> torch.Tensor:
+    """``_running_mean_bf16`` for E operands at once: parts [E, P, C] f32 per-batch sums, counts
+    [E][P] tokens.  Each step is the op the per-operand form issues with Python-int scalars on the
+    device -- bf16(f32(m) * c), bf16 + bf16, and the division by a scalar as a product with its f32
+    reciprocal (PyTorch's GPU kernel for a tensor / CPU-scalar division) -- taken with per-operand
+    f32 factors, so every row is bit-identical to the per-operand loop.  Operands without tokens
+    give 0."""
+    import numpy as np
+    E, P, C = parts.shape
+    dev = parts.device
+    m = torch.zeros(E, C, dtype=torch.bfloat16, device=dev)
+    seen = np.zeros(E, dtype=np.int64)
+    for j in range(P):
+        n = np.array([counts[e][j] for e in range(E)], dtype=np.int64)
+        live = n > 0
+        if not live.any():
+            continue
+        first = live & (seen == 0)
+        upd = live & (seen > 0)
+        inv = np.ones(E, dtype=np.float32)
+        inv[live] = np.float32(1.0) / (seen[live] + n[live]).astype(np.float32)
+        cf = seen.astype(np.float32)
+        sb = parts[:, j].to(torch.bfloat16)
+        t = (m.float() * torch.from_numpy(cf).to(dev)[:, None]).to(torch.bfloat16) + sb
+        t = torch.where(torch.from_numpy(first).to(dev)[:, None], sb, t)
+        new = (t.float() * torch.from_numpy(inv).to(dev)[:, None]).to(torch.bfloat16)
+        m = torch.where(torch.from_numpy(first | upd).to(dev)[:, None], new, m)
+        seen = seen + np.where(live, n, 0)
+    return m
+
+
 def _grid_scales_bf16(x_mean: torch.Tensor, w_mean: Optional[torch.Tensor], ratio: float, duo: bool,
                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """One grid point's scale vector(s) evaluated in bf16 as torch evaluates llmcompressor's
@@ -375,8 +406,9 @@ class _AbsMean:
             for x in xs:
                 self.add(x)
             return
-        parts = {id(x): torch.zeros(x.shape[-1], dtype=torch.float32, device=x.device) for x in live}
-        counts = dict(zip((id(x) for x in live), ops.awq_absmean_segments(live, [parts[id(x)] for x in live])))
+        buf = torch.zeros(len(live), live[0].shape[-1], dtype=torch.float32, device=live[0].device)
+        parts = {id(x): buf[i] for i, x in enumerate(live)}
+        counts = dict(zip((id(x) for x in live), ops.awq_absmean_segments(live, list(buf))))
         for x in xs:
             if not x.numel():
                 self.add(x)
@@ -1009,8 +1041,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         else:
             ei = experts[id(b0.module)]
             am = _AbsMean(bf16=bf16)
-            for i in range(n_batches):
-                am.add(_virtual_input(ei, b0, i))
+            am.add_samples([_virtual_input(ei, b0, i) for i in range(n_batches)])
             if am.count == 0:  # expert never routed to (moe_calibrate_all_experts=False)
                 log.info("AWQ: skipping mapping %s (no calibration tokens)", r.smooth_name)
                 return None
@@ -1135,16 +1166,31 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         wm = torch.empty_like(xm)
         hs = [torch.cat(h) if len(h) > 1 else h[0] for h in hid]  # all tokens of an expert: [T, I]
         del hid
-        for k, ref in enumerate(refs):
-            am = _AbsMean(bf16=bf16)
-            if bf16:  # one sum per calibration batch: the batches' token runs of the expert
-                counts = [ei.tokens(i, ref.index[0]).shape[0] for i in range(n_batches)]
-                for piece in torch.split(hs[k], counts):
-                    am.add(piece)
-            else:
+        if bf16:
+            # one sum per calibration batch (the batches' token runs of each expert), all experts'
+            # runs in segmented launches; the running means of all experts at once
+            counts = [[ei.tokens(i, ref.index[0]).shape[0] for i in range(n_batches)] for ref in refs]
+            parts = torch.zeros(len(refs), n_batches, cols, dtype=torch.float32, device=w2.device)
+            pieces, outs = [], []
+            for k in range(len(refs)):
+                for i, piece in enumerate(torch.split(hs[k], counts[k])):
+                    if piece.numel():
+                        pieces.append(piece)
+                        outs.append(parts[k, i])
+            ops.awq_absmean_segments(pieces, outs)
+            xm.copy_(_running_means_bf16(parts, counts))
+            # each expert's w2 is a balance layer of its own: bf16(column sum) / rows
+            wsums = torch.zeros(len(refs), cols, dtype=torch.float64, device=w2.device)
+            gs = _group_size_for_mean(a, cols)
+            rows = ops.awq_weight_mean_segments([ref.weight for ref in refs], gs, list(wsums))
+            assert len(set(rows)) == 1
+            wm.copy_(wsums.to(torch.bfloat16) / rows[0])
+        else:
+            for k, ref in enumerate(refs):
+                am = _AbsMean(bf16=bf16)
                 am.add(hs[k])
-            xm[k] = am.mean()
-            wm[k] = _w_mean([[ref]], quantized, cols, bf16, w2.device)
+                xm[k] = am.mean()
+                wm[k] = _w_mean([[ref]], quantized, cols, bf16, w2.device)
         # one GEMM per expert and grid point over all its tokens (2-D GEMMs: the path every
         # other mapping uses)
         w0 = torch.stack([w2[e] for e in es])  # [k, H, I] (pre-search weights)

@@ -130,3 +130,26 @@ def test_hip_awq_pipeline_matches_bf16_fixture(cuda):
     sm = w.clone()
     ops.scale_columns_(sm, f["scales"][int(f["best"])].float().to(cuda), divide=False)
     _bits_eq(sm.cpu(), f["smoothed"])
+
+
+@pytest.mark.gpu
+def test_running_means_batched_equals_per_operand_gpu():
+    """awq._running_means_bf16 (all experts of an expert search at once) == awq._running_mean_bf16
+    per expert on the device, bit for bit: ragged token counts, batches an expert never saw
+    (count 0, incl. its first batches), sums across many binades."""
+    from quantizers_amd import awq
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(8)
+    E, P, C = 37, 16, 768
+    counts = torch.randint(0, 300, (E, P), generator=g)
+    counts[counts < 60] = 0
+    counts[3, :5] = 0
+    counts[5, :] = 0
+    counts[5, 9] = 1
+    scale = 10.0 ** torch.empty(E, P, C).uniform_(-3, 2, generator=g)
+    parts = (torch.rand(E, P, C, generator=g) * scale * counts[:, :, None].clamp(min=1)).float().to(dev)
+    cl = counts.tolist()
+    got = awq._running_means_bf16(parts, cl)
+    for e in range(E):
+        want = awq._running_mean_bf16([(parts[e, j], cl[e][j]) for j in range(P)])
+        assert torch.equal(got[e].view(torch.int16), want.view(torch.int16)), e

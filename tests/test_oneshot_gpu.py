@@ -726,6 +726,70 @@ def test_expert_w3_w2_awq_matches_oracle(cuda, calibrate_all):
         _eq(experts.gate_up_proj.data[e, :64], gu0[e, :64], "w1 untouched")
 
 
+@pytest.mark.parametrize("calibrate_all", [True, False])
+def test_expert_w3_w2_awq_bf16_batched_statistics(cuda, calibrate_all):
+    """D8 bf16 reading on the expert w3 -> w2 searches, whose statistics are computed for all
+    experts of a search at once (segmented absmean over every expert's per-batch token runs, the
+    batched bf16 running mean, segmented w_mean): each expert's smoothing equals bf16(w2 * s) with s
+    from the per-expert computation (one absmean call per batch, the per-expert running mean, one
+    w_mean call), and the 20 losses follow the literal restatement."""
+    import torch.nn.functional as F
+    from quantizers_amd import awq as awq_mod
+    from quantizers_amd.awq import awq_layer
+    from quantizers_amd.recipe import AWQMapping
+    from quantizers_amd.quantization import QuantizationArgs
+    m = _minimax(layers=1, experts=4).to(cuda)
+    layer = m.model.layers[0]
+    experts = layer.mlp.experts
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=32)
+    pre = "model.layers.0.block_sparse_moe.experts"
+    quantized = {f"{pre}.{e}.{p}": a for e in range(4) for p in ("w1", "w2", "w3")}
+    from quantizers_amd.oneshot import _capture_layer0_inputs, _batches
+    inputs = _capture_layer0_inputs(m, m.model.layers, _batches(_calib(n=3, s=48, vocab=256), None, None, cuda))
+    seen = []
+    h = experts.register_forward_pre_hook(lambda mod, args: seen.append((args[0].clone(), args[1].clone())))
+    with torch.no_grad():
+        for args, kw in inputs:
+            layer(*args, **kw)
+    h.remove()
+    gu0, down0 = experts.gate_up_proj.data.clone(), experts.down_proj.data.clone()
+    rep = awq_layer(layer, "model.layers.0", inputs, [AWQMapping("re:.*w3$", ["re:.*w2$"])], quantized,
+                    mtype="minimax_m2", calibrate_all_experts=calibrate_all, awq_dtype="bf16")
+    oa = ct.QArgs(group_size=32)
+    for e in range(4):
+        with torch.no_grad():
+            hs = []
+            for x, topk in seen:
+                if not calibrate_all:
+                    x = x[(topk == e).any(-1)]
+                g, u = F.linear(x, gu0[e]).chunk(2, dim=-1)
+                hs.append(experts.act_fn(g) * u)
+        am = awq_mod._AbsMean(bf16=True)
+        for t in hs:
+            am.add(t)
+        ws = torch.zeros(down0.shape[2], dtype=torch.float64, device=cuda)
+        n = ops.awq_weight_mean_accum(down0[e], 32, ws)
+        wm = ws.to(torch.bfloat16) / n
+        r = rep[f"{pre}.{e}.w3"]
+        s = awq_mod._grid_scales_bf16(am.mean(), wm, r["best_ratio"], True)
+        _eq(experts.down_proj.data[e], (down0[e].float() * s.view(1, -1)).to(torch.bfloat16), f"w2 smoothed {e}")
+        prev = None
+        for t in hs:
+            if t.shape[0]:
+                prev = ct.awq_accumulate_mean_literal(t.cpu(), prev)
+        w2 = down0[e].cpu()
+        w_lit = ct.awq_layer_means_literal([w2], oa)
+        ref_out = [F.linear(t, down0[e]) for t in hs]
+        hist = []
+        for i in range(20):
+            sl = ct.awq_grid_scales_literal(prev[0], w_lit, i / 20, True)
+            wq = ct.awq_fake_quant_scaled_literal(w2, sl, oa).to(cuda)
+            got = [F.linear(t, wq) for t in hs]
+            hist.append(sum((p - q).float().pow(2).sum().item() for p, q in zip(ref_out, got)) /
+                        sum(p.numel() for p in ref_out))
+        torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(hist), rtol=5e-3, atol=1e-12)
+
+
 def _awq_rank(rank, world, port, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
