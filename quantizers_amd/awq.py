@@ -87,29 +87,36 @@ def _running_means_bf16(parts: torch.Tensor, counts: List[List[int]]) -> torch.T
     [E][P] tokens.  Each step is the op the per-operand form issues with Python-int scalars on the
     device -- bf16(f32(m) * c), bf16 + bf16, and the division by a scalar as a product with its f32
     reciprocal (PyTorch's GPU kernel for a tensor / CPU-scalar division) -- taken with per-operand
-    f32 factors, so every row is bit-identical to the per-operand loop.  Operands without tokens
-    give 0."""
+    f32 factors, so every row is bit-identical to the per-operand loop.  The factors of all steps
+    go to the device in one pinned, non-blocking copy (a pageable copy per step would make the
+    host wait for the stream).  Operands without tokens give 0."""
     import numpy as np
     E, P, C = parts.shape
     dev = parts.device
-    m = torch.zeros(E, C, dtype=torch.bfloat16, device=dev)
+    n = np.asarray(counts, dtype=np.int64).reshape(E, P)
+    fac = np.zeros((P, 4, E), dtype=np.float32)  # [step][c, 1/(c+n), first, apply][operand]
     seen = np.zeros(E, dtype=np.int64)
+    steps = []
     for j in range(P):
-        n = np.array([counts[e][j] for e in range(E)], dtype=np.int64)
-        live = n > 0
+        live = n[:, j] > 0
         if not live.any():
             continue
-        first = live & (seen == 0)
-        upd = live & (seen > 0)
-        inv = np.ones(E, dtype=np.float32)
-        inv[live] = np.float32(1.0) / (seen[live] + n[live]).astype(np.float32)
-        cf = seen.astype(np.float32)
+        fac[j, 0] = seen.astype(np.float32)
+        fac[j, 1] = 1.0
+        fac[j, 1, live] = np.float32(1.0) / (seen[live] + n[live, j]).astype(np.float32)
+        fac[j, 2] = live & (seen == 0)
+        fac[j, 3] = live
+        seen = seen + np.where(live, n[:, j], 0)
+        steps.append(j)
+    f = torch.from_numpy(fac)
+    if dev.type == "cuda":
+        f = f.pin_memory().to(dev, non_blocking=True)
+    m = torch.zeros(E, C, dtype=torch.bfloat16, device=dev)
+    for j in steps:
+        cf, inv, first, apply = (f[j, k][:, None] for k in range(4))
         sb = parts[:, j].to(torch.bfloat16)
-        t = (m.float() * torch.from_numpy(cf).to(dev)[:, None]).to(torch.bfloat16) + sb
-        t = torch.where(torch.from_numpy(first).to(dev)[:, None], sb, t)
-        new = (t.float() * torch.from_numpy(inv).to(dev)[:, None]).to(torch.bfloat16)
-        m = torch.where(torch.from_numpy(first | upd).to(dev)[:, None], new, m)
-        seen = seen + np.where(live, n, 0)
+        t = torch.where(first > 0, sb, (m.float() * cf).to(torch.bfloat16) + sb)
+        m = torch.where(apply > 0, (t.float() * inv).to(torch.bfloat16), m)
     return m
 
 
