@@ -307,7 +307,7 @@ def _start_warmup(model: nn.Module, device, seq_len: int) -> Optional[threading.
     """First-call costs of the capture forward, paid on a helper thread while the model moves to
     the device: the rotary embedding's f32 batched matmul ([1, head_dim / 2, 1] @ [1, 1, T]:
     0.18 s on its first call, the BLAS library's set-up), its cat / cos / sin (0.02 s) and a bf16
-    linear (0.04 s) (`scripts/first_call_probe.py`).  Nothing it computes is used."""
+    linear (0.04 s) (`scripts/first_call_probe.py`), and D8's bf16 grid ops.  Nothing it computes is used."""
     if not WARMUP or torch.device(device).type != "cuda":
         return None
     cfg = getattr(model, "config", None)
@@ -322,6 +322,14 @@ def _start_warmup(model: nn.Module, device, seq_len: int) -> Optional[threading.
         e.cos(), e.sin()
         x = torch.ones(16, 256, device=device, dtype=torch.bfloat16)
         torch.nn.functional.linear(x, x)
+        # D8's bf16 grid formula (pow / clamp / amax / amin / sqrt on bf16; 0.16 s of first calls
+        # on layer 0 otherwise, profiles/r05s_phases_bf16.log) and running mean
+        from . import awq as awq_mod
+        xm = torch.ones(2, 256, device=device, dtype=torch.float32)
+        for r in (0.0, 0.05, 0.5):
+            awq_mod._grid_scales_bf16(xm, xm, r, True)
+            awq_mod._grid_scales_bf16(xm[0], xm[0], r, False)
+        awq_mod._running_mean_bf16([(xm[0], 3), (xm[1], 5)])
         torch.cuda.synchronize(device)
 
     th = threading.Thread(target=run, name="qz-warmup", daemon=True)
