@@ -168,7 +168,7 @@ namespace qz {
 bool block_fp8_ok(const BlockFp8Job& J) {
   if (J.rows <= 0 || J.cols <= 0 || J.rows % 128 || J.cols % 128 || J.n <= 0 || J.n > 65535) return false;
   if (J.ld_row < J.cols || J.ld_row % 8 || J.ld_row > (1 << 22)) return false;  // 32-bit offsets in a strip
-  if (J.cols > (1 << 24)) return false;
+  if (J.cols > (1 << 24) || (J.rows / 128) * (J.cols / 128) > INT32_MAX) return false;  // grid.x, scale index
   if (J.tab) return aligned(J.tab, 8);
   if (!aligned(J.w, 16) || !aligned(J.q_out, 16) || !aligned(J.s_out, 2)) return false;
   return J.n == 1 || J.ld_batch % 8 == 0;

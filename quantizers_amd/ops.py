@@ -713,8 +713,10 @@ def awq_absmean_segments(xs: List[torch.Tensor], sums: List[torch.Tensor]) -> Li
         return []
     for x, o in zip(xs, sums):
         _check_dev(x, "activations")
-        if x.dtype != torch.bfloat16 or x.numel() == 0 or o.dtype != torch.float32 or x.shape[-1] != xs[0].shape[-1]:
-            raise ValueError("awq_absmean_segments: non-empty bf16 operands of one width, float32 sums")
+        if x.dtype != torch.bfloat16 or x.numel() == 0 or o.dtype != torch.float32 or x.shape[-1] != xs[0].shape[-1] \
+                or o.numel() != x.shape[-1] or not o.is_contiguous() or o.device != x.device:
+            raise ValueError("awq_absmean_segments: non-empty bf16 operands of one width, contiguous float32 sums "
+                             "of that width on the same device")
     return _segments("qz_awq_absmean_segments_workspace_size", "qz_awq_absmean_accum_segments",
                      awq_absmean_accum, xs, sums)
 
@@ -727,8 +729,10 @@ def awq_weight_mean_segments(ws: List[torch.Tensor], group_size: int, wsums: Lis
         return []
     for w, o in zip(ws, wsums):
         _check_dev(w, "weight")
-        if w.dtype != torch.bfloat16 or w.numel() == 0 or o.dtype != torch.float64 or w.shape[-1] != ws[0].shape[-1]:
-            raise ValueError("awq_weight_mean_segments: non-empty bf16 weights of one width, float64 sums")
+        if w.dtype != torch.bfloat16 or w.numel() == 0 or o.dtype != torch.float64 or w.shape[-1] != ws[0].shape[-1] \
+                or o.numel() != w.shape[-1] or not o.is_contiguous() or o.device != w.device:
+            raise ValueError("awq_weight_mean_segments: non-empty bf16 weights of one width, contiguous float64 sums "
+                             "of that width on the same device")
     g = int(group_size)
     return _segments("qz_awq_weight_mean_segments_workspace_size", "qz_awq_weight_mean_accum_segments",
                      lambda w, o: awq_weight_mean_accum(w, g, o), ws, wsums, g)

@@ -44,3 +44,13 @@ def test_grid_scales_bf16_matches_literal_oracle(duo):
 def test_awq_dtype_validated():
     with pytest.raises(ValueError):
         awq.awq_layer(torch.nn.Module(), "x", [], [], {}, awq_dtype="fp16")
+
+
+def test_stats_segments_validate_arguments():
+    """The segmented statistics wrappers reject operands the C side must never see (checked on
+    the host before any launch)."""
+    from quantizers_amd import ops
+    x = torch.zeros(4, 64, dtype=torch.bfloat16)
+    with pytest.raises(ValueError):  # host tensors
+        ops.awq_absmean_segments([x], [torch.zeros(64)])
+    assert ops.awq_absmean_segments([], []) == [] and ops.awq_weight_mean_segments([], 128, []) == []
