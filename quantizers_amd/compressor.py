@@ -137,33 +137,6 @@ def compression_units(model: nn.Module) -> Tuple[List[CompressUnit], Dict[str, t
     return units, raw
 
 
-ROW_BLOCKS = True  # merge the launches of one scheme and column count over row blocks (_RowBlocks)
-ROW_BLOCK_MIN = 256  # smallest row block (rows) a merged launch may use
-
-
-class _RowBlocks:
-    """One grouped launch over the row blocks of weights of one scheme and column count: each
-    weight's outputs are allocated whole, and the launch table holds row-block views of the
-    weights and of those outputs (all blocks [rb, cols])."""
-
-    def __init__(self, items, rb: int):
-        self.items, self.rb = items, rb
-
-    def launch(self, device):
-        a = self.items[0][0].scheme.weights
-        int_q, fmt = ops._compress_plan(a, self.items[0][0].scheme.input_activations is not None)
-        full, part, outs = [], [], []
-        for u, w in self.items:
-            o = ops.alloc_outputs(tuple(w.shape), a, fmt, device)
-            full.append((u, w, o))
-            for r0 in range(0, w.shape[0], self.rb):
-                part.append((u, w[r0:r0 + self.rb]))
-                outs.append({k: (v[r0:r0 + self.rb] if v is not None and k != "global_scale" else v)
-                             for k, v in o.items()})
-        gq = ops.GroupedQuantize([w for _, w in part], a, fmt, outs=outs)
-        return (gq, part, a, int_q, fmt, full)
-
-
 class CompressionPlan:
     """Prepared kernel launches for a set of compression units whose weights are on ``device``
     (staged there when the model is host-resident).  Dense units of one scheme and shape are ONE
@@ -176,7 +149,7 @@ class CompressionPlan:
 
     def __init__(self, units: Sequence[CompressUnit], device, stager=None):
         self.device = torch.device(device)
-        self.grouped = []  # (GroupedQuantize, [(unit, weight or row block)], args, int_q, fmt, [(unit, weight, outs)])
+        self.grouped = []  # (GroupedQuantize, [(unit, weight)], args, int_q, fmt)
         self.singles = []  # (unit, weight, preallocated outputs, args, int_q, fmt)
         buckets: Dict[tuple, list] = {}
         self.params = 0
@@ -211,11 +184,7 @@ class CompressionPlan:
                 buckets.setdefault(key, []).append((u, w))
             else:
                 self.singles.append((u, w, ops.alloc_outputs(tuple(w.shape), a, fmt, self.device), a, int_q, fmt))
-        buckets = self._merge_row_blocks(buckets) if ROW_BLOCKS else buckets
         for items in buckets.values():
-            if isinstance(items, _RowBlocks):
-                self.grouped.append(items.launch(self.device))
-                continue
             a = items[0][0].scheme.weights
             int_q, fmt = ops._compress_plan(a, items[0][0].scheme.input_activations is not None)
             if len({tuple(w.shape) for _, w in items}) > 8:  # at most 8 shapes per launch
@@ -231,37 +200,11 @@ class CompressionPlan:
                 seen.add(shp)
             for part in parts:
                 gq = ops.GroupedQuantize([w for _, w in part], a, fmt)
-                self.grouped.append((gq, part, a, int_q, fmt, [(u, w, q) for (u, w), q in zip(part, gq.outs)]))
+                self.grouped.append((gq, part, a, int_q, fmt))
         self._ready = None  # completion of the staging copies: every run() waits for it
         if staged:
             self._ready = torch.cuda.Event()
             self._ready.record(stager.stream)
-
-    @staticmethod
-    def _merge_row_blocks(buckets: Dict[tuple, list]) -> Dict[tuple, object]:
-        """Buckets of one group-strategy scheme and column count (several shapes: Qwen3-4B's q, k, v,
-        gate and up are all [*, 2560]) become ONE uniform launch over row blocks of the gcd of
-        their row counts: a group never spans rows, so a weight is the concatenation of its row
-        blocks' outputs (zero points are unpacked int8 rows until the writer packs them)."""
-        import math
-        merged: Dict[tuple, list] = {}
-        for key, items in buckets.items():
-            a = items[0][0].scheme.weights
-            blockable = (a.strategy == "group" and not a.is_nvfp4 and not ops.is_fp8_block128(a))
-            mkey = ("rows", key[0], key[1][1]) if blockable else key
-            merged.setdefault(mkey, []).extend(items)
-        out: Dict[tuple, object] = {}
-        for key, items in merged.items():
-            shapes = {tuple(w.shape) for _, w in items}
-            rb = 0
-            for r, _ in shapes:
-                rb = math.gcd(rb, r)
-            if key[0] != "rows" or len(shapes) < 2 or rb % 8 or rb < ROW_BLOCK_MIN:
-                for shp in sorted(shapes):  # as before: one bucket per shape
-                    out[(key, shp)] = [uw for uw in items if tuple(uw[1].shape) == shp]
-                continue
-            out[key] = _RowBlocks(items, rb)
-        return out
 
     @property
     def launches(self) -> int:
@@ -309,8 +252,8 @@ class CompressionPlan:
     def tensors(self) -> Dict[str, torch.Tensor]:
         """The on-disk tensors of every unit (device tensors; ``weight_shape`` on the host)."""
         out: Dict[str, torch.Tensor] = {}
-        for gq, part, a, int_q, fmt, full in self.grouped:
-            for u, w, q in full:
+        for gq, part, a, int_q, fmt in self.grouped:
+            for (u, w), q in zip(part, gq.outs):
                 for k, v in ops._compressed_tensors(q, tuple(w.shape), a, int_q, fmt).items():
                     out[f"{u.refs[0].name}.{k}"] = v
         for u, w, q, a, int_q, fmt in self.singles:

@@ -869,7 +869,7 @@ def test_reentrant_from_host_threads(cuda):
 
 def test_whole_model_plan_equals_per_weight(cuda):
     """The headline workload in full: the product's CompressionPlan over all 252 Qwen3-4B linears
-    (3 grouped launches, the bench's step) gives every on-disk tensor bit-identical to the
+    (5 grouped launches, the bench's step) gives every on-disk tensor bit-identical to the
     per-weight launch of the same weight (itself oracle-checked at full size above), and one
     weight per shape matches the plain-C oracle outright."""
     import os
@@ -877,14 +877,12 @@ def test_whole_model_plan_equals_per_weight(cuda):
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     import qref
-    from quantizers_amd import compressor
     from quantizers_amd.compressor import CompressionPlan, compression_units
     torch.manual_seed(3)
     model = bench.build_model(cuda)
     units, _ = compression_units(model)
     plan = CompressionPlan(units, cuda)
-    # q / k / v / gate / up ([*, 2560]) as one launch over 512-row blocks, o and down one each
-    assert plan.launches == (3 if compressor.ROW_BLOCKS else 5) and len(units) == 252
+    assert plan.launches == 5 and len(units) == 252
     plan.run()
     got = plan.tensors()
     seen = set()
