@@ -134,9 +134,10 @@ int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* 
  *   table[i] = weight i (bf16, dense, 16-B aligned), table[n+i] = its codes, table[2n+i] = its
  *   scales, table[3n+i] = its int8 zero points (required for asymmetric schemes, else 0).
  * Output layouts are exactly qz_quantize's with batch = 1.  No weight may alias any output.
- * Single-pass group schemes only (GROUP / TENSOR_GROUP with a power-of-two group 8..512, int /
- * FP8 / MXFP4 / FP4, not NVFP4 and not fake-quant): anything else returns QZ_ERR_FORMAT and the
- * caller uses qz_quantize_many.  n <= 65535.  No workspace.
+ * Single-pass group schemes (GROUP / TENSOR_GROUP with a power-of-two group 8..512, int / FP8 /
+ * MXFP4 / FP4, not NVFP4 and not fake-quant) and, from round 5, FP8_BLOCK 128 x 128 (e4m3 codes,
+ * rows and cols multiples of 128; the strip kernel of qz_block.hip, table[3n+i] unused): anything
+ * else returns QZ_ERR_FORMAT and the caller uses qz_quantize_many.  n <= 65535.  No workspace.
  */
 int qz_quantize_grouped(int64_t n, const uint64_t* table, int64_t rows, int64_t cols,
                         const qz_args* a, int32_t out_fmt, qz_stream_t stream);
