@@ -54,3 +54,30 @@ def test_stats_segments_validate_arguments():
     with pytest.raises(ValueError):  # host tensors
         ops.awq_absmean_segments([x], [torch.zeros(64)])
     assert ops.awq_absmean_segments([], []) == [] and ops.awq_weight_mean_segments([], 128, []) == []
+
+
+def test_running_means_batched_cpu_semantics():
+    """awq._running_means_bf16 takes, per operand and batch, bf16(f32(m) * c), the bf16 sum and
+    the product with the f32 reciprocal of the running count -- restated here step by step with
+    NumPy f32 reciprocals (the GPU test compares it with the per-operand device loop)."""
+    import numpy as np
+    g = torch.Generator().manual_seed(5)
+    E, P, C = 6, 7, 32
+    counts = torch.randint(0, 6, (E, P), generator=g)
+    counts[2] = 0
+    counts[2, 5] = 4
+    counts[4] = 0  # an operand that never saw a token: 0
+    parts = torch.rand(E, P, C, generator=g) * 300
+    got = awq._running_means_bf16(parts, counts.tolist())
+    for e in range(E):
+        m, c = torch.zeros(C, dtype=torch.bfloat16), 0
+        for j in range(P):
+            n = int(counts[e, j])
+            if n == 0:
+                continue
+            sb = parts[e, j].to(torch.bfloat16)
+            inv = float(np.float32(1.0) / np.float32(c + n))
+            t = sb if c == 0 else (m.float() * float(c)).to(torch.bfloat16) + sb
+            m = (t.float() * inv).to(torch.bfloat16)
+            c += n
+        assert torch.equal(got[e].view(torch.int16), m.view(torch.int16)), e
