@@ -408,19 +408,19 @@ class _AbsMean:
         each sample's total from zero, bit-identical to its own call, then combined as the
         sequential adds combine them (f32 sum += total in sample order; bf16: one part each)."""
         xs = [x.detach() if x.dtype == torch.bfloat16 else x.detach().to(torch.bfloat16) for x in xs]
-        live = [x for x in xs if x.numel()]
+        live = [i for i, x in enumerate(xs) if x.numel()]
         if not live:
             for x in xs:
                 self.add(x)
             return
-        buf = torch.zeros(len(live), live[0].shape[-1], dtype=torch.float32, device=live[0].device)
-        parts = {id(x): buf[i] for i, x in enumerate(live)}
-        counts = dict(zip((id(x) for x in live), ops.awq_absmean_segments(live, list(buf))))
-        for x in xs:
+        buf = torch.zeros(len(live), xs[live[0]].shape[-1], dtype=torch.float32, device=xs[live[0]].device)
+        counts = ops.awq_absmean_segments([xs[i] for i in live], list(buf))
+        slot = {i: k for k, i in enumerate(live)}
+        for i, x in enumerate(xs):
             if not x.numel():
                 self.add(x)
                 continue
-            part, n = parts[id(x)], counts[id(x)]
+            part, n = buf[slot[i]], counts[slot[i]]
             if self.bf16:
                 self.parts.append((part, n))
             else:
