@@ -9,10 +9,10 @@
 // One pass, one HBM read.  A workgroup of 256*NB threads covers a 128-row x (128*NB)-column
 // strip: NB horizontally adjacent blocks of one block row, held in registers (8 units of 8 bf16
 // per thread).  Thread t owns column unit t % (16*NB) of rows t / (16*NB) + 16*i, i < 8, so one
-// wave-load reads (4/NB) rows x NB*256 contiguous bytes: NB = 4 reads whole 1 KiB row pieces
-// where the round-1 tile kernel (k_tile_fast, one block per workgroup) read 256-B pieces.  Block
-// |max| on the raw bf16 words (v_pk_max_u16), DPP within the 16 lanes of a block row, then across
-// the 4*NB waves through LDS.  The e4m3 codes of two lanes holding adjacent units of one row are
+// wave-load reads (4/NB) rows x NB*256 contiguous bytes (the default NB = 2: 512-B row pieces;
+// the round-1 tile kernel, k_tile_fast with one block per workgroup, read 256-B pieces).  Block
+// |max| on the raw bf16 words (v_pk_max_u16), DPP within the 16 lanes of a block row, lane
+// shuffles across the rows a wave holds, then across the 4*NB waves through LDS.  The e4m3 codes of two lanes holding adjacent units of one row are
 // exchanged by one DPP swap so every lane writes 16 B (even lanes the even rows of a pair, odd
 // lanes the odd rows): 16-B stores instead of 8-B ones.  Everything is shifts: no divisions but the
 // workgroup's block coordinates (scalar).
