@@ -151,14 +151,33 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def _timed(fn, reps=3):
-    fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(reps):
+PASSES = 5  # event-timed passes per secondary leg; the median is reported
+
+
+WARM_S = 0.08  # untimed load before a leg's passes: the clocks settle ~35 ms into a load (r05j_step_ramp)
+
+
+def _event_median(fn, stream, passes=PASSES, warm=1, warm_s=WARM_S):
+    """Median seconds of ``passes`` calls of ``fn`` (each enqueues one whole pass on ``stream``),
+    each between its own pair of HIP events on that stream, after at least ``warm`` untimed calls
+    and ``warm_s`` seconds of them (a leg that starts from an idle GPU otherwise times the clock
+    ramp: 19.4 -> 17.5 us per weight over 7 grouped passes, profiles/r06e_bench_compare.txt);
+    also returns every pass's seconds."""
+    t0, i = time.perf_counter(), 0
+    while i < warm or time.perf_counter() - t0 < warm_s:
         fn()
-    torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / reps
+        i += 1
+        if i >= warm:
+            torch.cuda.synchronize()
+    ts = []
+    for _ in range(passes):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e-3)
+    return sorted(ts)[len(ts) // 2], ts
 
 
 def mixed_plan_leg(ops, dev, stream, steps=10):
@@ -175,25 +194,15 @@ def mixed_plan_leg(ops, dev, stream, steps=10):
     model = build_model(dev, MIXED_RECIPE)
     units, _ = compression_units(model)
     plan = CompressionPlan(units, dev)
-    for _ in range(3):
-        plan.run(stream)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(steps):
-        plan.run(stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    s = e0.elapsed_time(e1) * 1e-3 / steps
+    def steps_pass():
+        for _ in range(steps):
+            plan.run(stream)
+    s, _ = _event_median(steps_pass, stream, warm=1)
+    s /= steps
     alg = plan.alg_bytes()
     per = []
     for gq, part, *_ in plan.grouped:
-        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        f0.record(stream)
-        gq.run(stream)
-        f1.record(stream)
-        torch.cuda.synchronize()
-        us = f0.elapsed_time(f1) * 1e3
+        us = _event_median(lambda gq=gq: gq.run(stream), stream, passes=11, warm=2)[0] * 1e6
         rb = sum(w.numel() * 2 for _, w in part)
         nb = rb + sum(t.numel() * t.element_size() for o in gq.outs for t in o.values() if t is not None)
         per.append({"scheme": "FP8_BLOCK 128x128" if ops.is_fp8_block128(gq.a) else
@@ -204,7 +213,8 @@ def mixed_plan_leg(ops, dev, stream, steps=10):
            "alg_bytes": alg, "alg_GBps": alg / s / 1e9, "frac": alg / s / 1e9 / HBM_PEAK_GBS,
            "read_frac": plan.params * 2 / s / 1e9 / HBM_PEAK_GBS, "per_launch": per,
            "recipe": "configs/recipes/mixed_fp8_block_awq_int4.yaml",
-           "timing": f"HIP events on the launch stream around {steps} CompressionPlan steps"}
+           "timing": f"HIP events on the launch stream around {steps} CompressionPlan steps, median of {PASSES} "
+                     f"such passes; per launch: one event pair per launch, median of 11"}
     del plan, units, model
     torch.cuda.empty_cache()
     return res
@@ -224,17 +234,25 @@ def other_configs(ops, QuantizationArgs, dev, gen, stream):
         dn = (torch.randn(128, 2048, 768, device=dev, generator=gen) * 0.02).to(torch.bfloat16)
         layers.append((gu, dn))
 
+    # outputs preallocated, every launch's arguments marshalled once (ops.PreparedQuantize): one
+    # ctypes call per launch, no allocation inside the timed passes
+    views = [w for gu, dn in layers for w in (gu[:, :768], gu[:, 768:], dn)]
+    preps = [ops.PreparedQuantize(w, mx, ops.alloc_outputs(tuple(w.shape), mx, None, dev)) for w in views]
+
     def moe_pass():
         for li in range(48):
-            gu, dn = layers[li % 4]
-            ops.quantize_weight(gu[:, :768], mx)
-            ops.quantize_weight(gu[:, 768:], mx)
-            ops.quantize_weight(dn, mx)
+            for j in range(3):
+                k = (li % 4) * 3 + j
+                preps[k].run(views[k], stream)
     npar = 48 * 128 * 3 * 768 * 2048
-    t = _timed(moe_pass, reps=2)
+    t, ts = _event_median(moe_pass, stream)
+    nb = npar * (2 + 0.5 + 1 / 32)
     res["qwen3_30b_a3b_experts_mxfp4"] = {"params": npar, "ms": t * 1e3, "params_per_s": npar / t,
-                                          "alg_GBps": npar * (2 + 0.5 + 1 / 32) / t / 1e9,
-                                          "frac": npar * (2 + 0.5 + 1 / 32) / t / 1e9 / HBM_PEAK_GBS}
+                                          "alg_GBps": nb / t / 1e9, "frac": nb / t / 1e9 / HBM_PEAK_GBS,
+                                          "ms_passes": [round(x * 1e3, 4) for x in ts],
+                                          "timing": f"HIP events around each whole pass (144 launches), median of "
+                                                    f"{PASSES}; outputs preallocated"}
+    del preps
     res["qwen3_30b_a3b_experts_nvfp4"] = nvfp4_experts_leg(ops, QuantizationArgs, layers, dev)
     del layers
     torch.cuda.empty_cache()
@@ -288,19 +306,10 @@ def nvfp4_experts_leg(ops, QuantizationArgs, layers, dev):
     nb = npar * NV_B_PER_PARAM + 48 * 3 * 128 * 4
     res = {"params": npar, "alg_bytes": nb, "kernel": "k_nv_absmax<false> + k_nv_encode<false> (qz_quantize_nvfp4)",
            "recipe": "reference configs/recipes/recipe_MoE_RTN_NVFP4.yaml (scheme NVFP4)",
-           "timing": "HIP events around one whole pass (144 fused parameters back to back), best of 3"}
+           "timing": "HIP events around each whole pass (144 fused parameters back to back), median of 7"}
     st = torch.cuda.current_stream(dev)
     for name, fn in (("fused", fused), ("fused_one_stream", fused_one_stream), ("two_pass", two_pass)):
-        fn()
-        torch.cuda.synchronize()
-        best = None
-        for _ in range(3):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            fn()
-            e1.record(st)
-            torch.cuda.synchronize()
-            best = e0.elapsed_time(e1) * 1e-3 if best is None else min(best, e0.elapsed_time(e1) * 1e-3)
+        best, _ = _event_median(fn, st, passes=7)
         gbps = nb / best / 1e9
         leg = {"ms": best * 1e3, "params_per_s": npar / best, "alg_GBps": gbps, "frac": gbps / HBM_PEAK_GBS,
                "read_frac": npar * 2 / best / 1e9 / HBM_PEAK_GBS,
@@ -333,36 +342,39 @@ def minimax_pass(ops, QuantizationArgs, dev, gen, world, rank):
         at = [(torch.randn(r, c, device=dev, generator=gen) * 0.02).to(torch.bfloat16) for r, c in attn]
         res_layers.append((gu, dn, at))
 
+    # every launch prepared once (outputs preallocated, arguments marshalled): one ctypes call each
+    launches = []
+    for gu, dn, at in res_layers:
+        lay = [(w, i4) for w in (gu[:, :inter], gu[:, inter:], dn)] + [(w, f8) for w in at]
+        launches.append([(w, ops.PreparedQuantize(w, a, ops.alloc_outputs(tuple(w.shape), a, None, dev)))
+                         for w, a in lay])
+    stream = torch.cuda.current_stream(dev)
+
     def run():
         for j, _ in enumerate(mine):
-            gu, dn, at = res_layers[j % 2]
-            ops.quantize_weight(gu[:, :inter], i4)
-            ops.quantize_weight(gu[:, inter:], i4)
-            ops.quantize_weight(dn, i4)
-            for w in at:
-                ops.quantize_weight(w, f8)
+            for w, prep in launches[j % 2]:
+                prep.run(w, stream)
 
-    run()
-    torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    t0 = time.perf_counter()
-    reps = 2
-    for _ in range(reps):
-        run()
-    torch.cuda.synchronize()
+    t, ts = _event_median(run, stream) if mine else (0.0, [])
     if world > 1:
         dist.barrier()
-    t = torch.tensor([(time.perf_counter() - t0) / reps], device=dev, dtype=torch.float64)
+    t = torch.tensor([t], device=dev, dtype=torch.float64)
     if world > 1:
         _all_reduce_max(t)
     t = t.item()
+    del launches
     p_exp = n_layers * n_exp * 3 * inter * hid
     p_att = n_layers * sum(r * c for r, c in attn)
     del res_layers
     torch.cuda.empty_cache()
     return {"params": p_exp + p_att, "ms": t * 1e3, "params_per_s": (p_exp + p_att) / t, "ranks": world,
             "alg_GBps": (p_exp * (2 + 0.5 + 2 / 32) + p_att * (2 + 1 + 2 / 32)) / t / 1e9,
+            "frac": (p_exp * (2 + 0.5 + 2 / 32) + p_att * (2 + 1 + 2 / 32)) / t / 1e9 / HBM_PEAK_GBS / world,
+            "ms_passes_this_rank": [round(x * 1e3, 4) for x in ts],
+            "timing": f"HIP events around each pass of the rank's layers (7 launches per layer, outputs "
+                      f"preallocated), median of {PASSES}, max over ranks",
             "sharding": "layers round-robin over ranks (strong scaling)"}
 
 
@@ -384,7 +396,7 @@ def _all_gather_into(out, inp):
         dist.all_gather_into_tensor(out, inp)
 
 
-def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream, n=40):
+def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream, n=60):
     """The AWQ kernels on the headline weight shape, each with its
     algorithmic bytes and achieved HBM GB/s (rotating the HBM-resident weight copies).
 
@@ -432,19 +444,14 @@ def awq_kernels(ops, QuantizationArgs, copies, dev, gen, stream, n=40):
         ("scale_columns (a6: W[:, c] *= s[c])",
          lambda i: ok(lib.qz_scale_columns(wp[i % nc], ROWS, COLS, COLS, P(s.data_ptr()), i & 1, st)), PARAMS * 4),
     ]:
-        for i in range(3):
-            fn(i)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for i in range(n):
-            fn(i)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / n
+        def batch(fn=fn):
+            for i in range(n):
+                fn(i)
+        t, _ = _event_median(batch, stream, passes=9)
+        us = t * 1e6 / n
         res[name] = {"us": us, "alg_bytes": nbytes, "GBps": nbytes / (us * 1e-6) / 1e9,
                      "frac": nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                     "timing": f"{n} launches back to back between one event pair"}
+                     "timing": f"{n} launches back to back between one event pair, median of 9 such passes"}
     del x
     return res
 
@@ -513,19 +520,14 @@ def synthetic_leg(ops, QuantizationArgs, dev, gen, stream, copies_n, k):
     many = prep.prepare_many(ws, outs=outs)
     res = {}
     for name, fn, launches in (("grouped", lambda: gq.run(stream), 1), ("per_weight", lambda: many(stream), k)):
-        for _ in range(3):
-            fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        fn()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        us_w = e0.elapsed_time(e1) * 1e3 / k
+        t, ts = _event_median(fn, stream, passes=max(PASSES, 7), warm=3)
+        us_w = t * 1e6 / k
         gbps = ALG_BYTES / (us_w * 1e-6) / 1e9
         res[name] = {"kernel": kernel_name(name == "grouped", (k if name == "grouped" else 1) * PARAMS * 2),
                      "weights": k, "launches": launches, "us_per_weight": us_w, "params_per_s": PARAMS / (us_w * 1e-6),
-                     "achieved_GBps": gbps, "frac": gbps / HBM_PEAK_GBS}
+                     "achieved_GBps": gbps, "frac": gbps / HBM_PEAK_GBS,
+                     "us_per_weight_passes": [round(x * 1e6 / k, 3) for x in ts],
+                     "timing": f"HIP events around each pass ({k} weights), median of {len(ts)} passes"}
     check = (copies[(k - 1) % copies_n][:256].cpu(), outs[k - 1]["codes"][:256].cpu(), outs[k - 1]["scale"][:256].cpu())
     del gq, many, prep, outs, ws
     return res, copies, check
@@ -541,7 +543,7 @@ def row_blocks(rows: int, world: int, align: int = 8):
     return [(min(r * blk, rows), min((r + 1) * blk, rows)) for r in range(world)], blk
 
 
-def row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank, reps=5):
+def row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank, reps=7):
     """BASELINE.md §2 multi-GPU row: the north-star synthetic weight [11008, 4096] int4-g128 split
     into ``world`` row blocks (``row_blocks``), rank r quantizing block r (strong scaling: the
     weight is fixed).  Every rank generates the same copies (seeded), keeps only its block.
@@ -574,17 +576,7 @@ def row_sharded_leg(ops, QuantizationArgs, dev, stream, world, rank, reps=5):
     if mine:
         outs = [ops.alloc_outputs((mine, COLS), a, None, dev) for _ in range(n)]
         gq = ops.GroupedQuantize(copies, a, outs=outs)
-        for _ in range(3):
-            gq.run(stream)
-        ts = []
-        for _ in range(reps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            gq.run(stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e3 / n)
-        us_copy = sorted(ts)[len(ts) // 2]
+        us_copy = _event_median(lambda: gq.run(stream), stream, passes=reps, warm=3)[0] * 1e6 / n
         del gq, outs
     t = torch.tensor([us_copy], device=dev, dtype=torch.float64)
     if world > 1:
@@ -852,20 +844,20 @@ def main():
               "how": "HIP events around 100 steps after 50 more untimed ones, right after the timed region; "
                      "informational (value and roofline use the W / K given)"}
 
-    # per-launch durations (untimed, after the regions above): each launch 5 times back to back,
+    # per-launch durations (untimed, after the regions above): each launch 11 times back to back,
     # one event pair per launch, the median (a single launch after a synchronize can catch a clock
     # transient)
     per_launch = []
     for gq, part, *_ in plan.grouped:
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(12)]
         evs[0].record(stream)
-        for i in range(5):
+        for i in range(11):
             gq.run(stream)
             evs[i + 1].record(stream)
         torch.cuda.synchronize()
         nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
                                                          for t in o.values() if t is not None)
-        us = sorted(evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(5))[2]
+        us = sorted(evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(11))[5]
         rb = sum(w.numel() * 2 for _, w in part)
         per_launch.append({"shapes": sorted({f"{r}x{c}" for r, c in gq.shapes}), "weights": gq.n,
                            "us": us, "alg_bytes": nb, "read_bytes": rb,

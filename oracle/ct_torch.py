@@ -412,27 +412,56 @@ def awq_fake_quant_scaled(w: torch.Tensor, s: torch.Tensor, a: QArgs) -> torch.T
 # ----------------------------------------------------------------------------------------
 # D8, the literal reading of SURVEY A.6 ("accumulation dtype = activation dtype"): every AWQ
 # statistic, grid scale and scaled weight in the weight / activation dtype (bf16), the loss an f32
-# sum per calibration batch.  Not the oracle's decision (awq_* above): used only to MEASURE what
-# that decision changes (tests/golden/d8_probe.py).  Op order as llmcompressor's
+# sum per calibration batch.  Since round 5 this is the oracle of the product's DEFAULT reading
+# (awq_dtype="bf16"; the fp32 reading's oracle is awq_* above).  Op order as llmcompressor's
 # _accumulate_mean / _compute_layer_means / _compute_best_scale / _compute_loss ([3P], unpinned).
+#
+# Device semantics: llmcompressor's sequential pipeline runs each layer -- and so
+# the activation hook's and _compute_layer_means' tensor ops -- on the accelerator.  The one op whose
+# bits depend on that is the division of a bf16 tensor by a Python number: torch's CPU kernel
+# divides (bf16(f32(a) / f32(n))), its GPU kernel multiplies by the f32 reciprocal of the scalar
+# (bf16(f32(a) * (1.0f / f32(n))), BinaryDivTrueKernel's CPU-scalar case).  device_division=True
+# restates the GPU form, the product's; False the CPU form.  Every other op here (bf16 x scalar
+# product, bf16 adds, pow, clamp, amax / amin) rounds f32 arithmetic to bf16 identically on both.
 # ----------------------------------------------------------------------------------------
-def awq_accumulate_mean_literal(x: torch.Tensor, prev=None):
+def div_scalar_bf16(t: torch.Tensor, n, device_division: bool) -> torch.Tensor:
+    """bf16 tensor / Python number as torch computes it on the GPU (reciprocal product,
+    ``device_division``) or on the CPU (true division)."""
+    if not device_division:
+        return t / n
+    import numpy as np
+    inv = float(np.float32(1.0) / np.float32(n))
+    return (t.float() * inv).to(t.dtype)
+
+
+def awq_accumulate_mean_literal(x: torch.Tensor, prev=None, device_division: bool = False):
     """Running mean of |x| over tokens in x's dtype: (prev_mean * prev_n + sum) / (prev_n + n),
     every op rounded to bf16 (the per-batch sum accumulates in f32 inside torch, rounded once)."""
     inp = x.reshape(-1, x.shape[-1]).abs()
-    s = inp.sum(0)
-    n = inp.shape[0]
-    if prev is None:
-        return s / n, n
-    pm, pc = prev
-    return (pm * pc + s) / (pc + n), pc + n
+    return awq_running_mean_from_sums_literal([(inp.sum(0), inp.shape[0])], prev, device_division)
 
 
-def awq_layer_means_literal(weights, a: QArgs) -> torch.Tensor:
+def awq_running_mean_from_sums_literal(parts, prev=None, device_division: bool = True):
+    """_accumulate_mean over per-batch column sums [(sum, n), ...] in batch order: each sum
+    rounded once to bf16 (a bf16 tensor's ``sum(0)`` accumulates in f32 and rounds once; an f32
+    sum given here, e.g. the absmean kernel's, is rounded here), then (prev_mean * prev_n + sum) /
+    (prev_n + n) in bf16.  Returns (mean, count); batches without tokens are skipped."""
+    for s, n in parts:
+        if n == 0:
+            continue
+        s = s.to(torch.bfloat16)
+        if prev is None:
+            prev = (div_scalar_bf16(s, n, device_division), n)
+        else:
+            pm, pc = prev
+            prev = (div_scalar_bf16(pm * pc + s, pc + n, device_division), pc + n)
+    return prev
+
+
+def awq_layer_means_literal(weights, a: QArgs, device_division: bool = False) -> torch.Tensor:
     """w_mean in the weight dtype: per layer a bf16 column sum, summed across layers in bf16,
     divided by the row count in bf16."""
-    total = 0
-    acc = None
+    parts = []
     for w in weights:
         n, k = w.shape
         g = {"tensor": w.numel(), "channel": k}.get(a.strategy, a.group_size)
@@ -440,10 +469,21 @@ def awq_layer_means_literal(weights, a: QArgs) -> torch.Tensor:
             g = k
         v = w.reshape(-1, g)
         v = (v.abs() / (v.abs().amax(dim=1, keepdim=True) + 1e-6)).reshape(n, k)
-        s = v.sum(0)
+        parts.append((v.sum(0), n))
+    return awq_layer_means_from_sums_literal(parts, device_division)
+
+
+def awq_layer_means_from_sums_literal(parts, device_division: bool = True) -> torch.Tensor:
+    """_compute_layer_means' combination of per-layer column sums [(sum, rows), ...] in the
+    mapping's balance order: each sum rounded once to bf16 (torch's bf16 ``sum(0)`` rounds its f32
+    accumulation once; the w_mean kernel's f64 sum is rounded here), added in bf16, divided by the
+    total row count in bf16."""
+    acc, total = None, 0
+    for s, n in parts:
+        s = s.to(torch.bfloat16)
         acc = s if acc is None else acc + s
         total += n
-    return acc / total
+    return div_scalar_bf16(acc, total, device_division)
 
 
 def awq_grid_scales_literal(x_mean: torch.Tensor, w_mean: torch.Tensor, ratio: float, duo: bool = True):

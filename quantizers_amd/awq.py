@@ -44,6 +44,7 @@ import threading
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
+import numpy as np
 import torch
 from torch import nn
 
@@ -69,17 +70,38 @@ AWQ_DTYPES = ("bf16", "fp32")
 AWQ_DTYPE = "bf16"
 
 
+def _div_count_bf16(t: torch.Tensor, n: int) -> torch.Tensor:
+    """bf16 tensor / a token or row count as torch's GPU kernel computes it (the product with the
+    f32 reciprocal of the count; DESIGN.md §4 D8 "device semantics"), written out so the bits do not
+    depend on the tensor's device (torch's CPU kernel divides)."""
+    return (t.float() * float(np.float32(1.0) / np.float32(n))).to(torch.bfloat16)
+
+
 def _running_mean_bf16(parts) -> Optional[torch.Tensor]:
     """llmcompressor's _accumulate_mean in bf16 over per-batch f32 sums [(sum [C], n), ...] in
-    batch order: m = s_0 / n_0, then m = (m * count + s_j) / (count + n_j)."""
+    batch order: m = s_0 / n_0, then m = (m * count + s_j) / (count + n_j), each division by a
+    count in torch's GPU form (``_div_count_bf16``; oracle: ct_torch.awq_running_mean_from_sums_literal
+    with device_division=True)."""
     m, c = None, 0
     for part, n in parts:
         if n == 0:
             continue
         sb = part.to(torch.bfloat16)
-        m = sb / n if m is None else (m * c + sb) / (c + n)
+        m = _div_count_bf16(sb if m is None else m * c + sb, c + n)
         c += n
     return m
+
+
+def _layer_means_bf16(parts) -> torch.Tensor:
+    """_compute_layer_means' bf16 combination of per-balance-layer column sums [(sum, rows), ...]
+    in balance order: each sum rounded once to bf16, added in bf16, / the total rows in torch's GPU
+    form (oracle: ct_torch.awq_layer_means_from_sums_literal, device_division=True)."""
+    acc, rows = None, 0
+    for part, n in parts:
+        sb = part.to(torch.bfloat16)
+        acc = sb if acc is None else acc + sb
+        rows += n
+    return _div_count_bf16(acc, rows)
 
 
 def _running_means_bf16(parts: torch.Tensor, counts: List[List[int]]) -> torch.Tensor:
@@ -144,8 +166,9 @@ PHASES: Dict[str, float] = {}  # phase name -> seconds, accumulated while PHASE_
 
 @contextlib.contextmanager
 def phase(name: str):
-    """Accumulate the synchronised wall time of a block under ``name`` (QZ_AWQ_PHASE_TIMING=1
-    only: the synchronisations perturb the overlap they measure, so it is a diagnostic mode)."""
+    """Accumulate the synchronised wall time of a block under ``name`` (only with the module
+    constant ``awq.PHASE_TIMING = True``: the synchronisations perturb the overlap they measure, so
+    it is a diagnostic mode)."""
     if not PHASE_TIMING:
         yield
         return
@@ -787,14 +810,10 @@ def _w_mean(groups: List[List[LinearRef]], quantized: Dict[str, QuantizationArgs
             wsum += part  # ((0 + v_0) + v_1) + ...: the sequential calls' f64 adds
             rows += n
         return (wsum / rows).float()
-    acc, rows = None, 0
     # every balance linear is a layer of its own (each expert slice too)
-    for part, n in _w_mean_parts([(ref.weight, _group_size_for_mean(quantized[ref.name], cols)) for ref in
-                                  (refs if refs is not None else [x for g in groups for x in g])], cols, device):
-        sb = part.to(torch.bfloat16)
-        acc = sb if acc is None else acc + sb
-        rows += n
-    return acc / rows
+    return _layer_means_bf16(_w_mean_parts([(ref.weight, _group_size_for_mean(quantized[ref.name], cols)) for ref in
+                                            (refs if refs is not None else [x for g in groups for x in g])],
+                                           cols, device))
 
 
 def _w_mean_parts(items: List[Tuple[torch.Tensor, int]], cols: int, device) -> List[Tuple[torch.Tensor, int]]:
@@ -1048,7 +1067,10 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
         else:
             ei = experts[id(b0.module)]
             am = _AbsMean(bf16=bf16)
-            am.add_samples([_virtual_input(ei, b0, i) for i in range(n_batches)])
+            # in chunks of one segmented launch: each batch's expert input is a fresh GEMM output,
+            # so only STATS_SEGS of them are alive at once (same sums, same order: ADVICE r05)
+            for i0 in range(0, n_batches, ops.STATS_SEGS):
+                am.add_samples([_virtual_input(ei, b0, i) for i in range(i0, min(i0 + ops.STATS_SEGS, n_batches))])
             if am.count == 0:  # expert never routed to (moe_calibrate_all_experts=False)
                 log.info("AWQ: skipping mapping %s (no calibration tokens)", r.smooth_name)
                 return None
@@ -1181,8 +1203,8 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             pieces, outs = [], []
             for k in range(len(refs)):
                 for i, piece in enumerate(torch.split(hs[k], counts[k])):
-                    if piece.numel():
-                        pieces.append(piece)
+                    if piece.numel():  # the segmented kernel reads bf16 (fp16 / fp32 models: ADVICE r05)
+                        pieces.append(piece if piece.dtype == torch.bfloat16 else piece.to(torch.bfloat16))
                         outs.append(parts[k, i])
             ops.awq_absmean_segments(pieces, outs)
             xm.copy_(_running_means_bf16(parts, counts))
@@ -1191,7 +1213,7 @@ def awq_layer(layer: nn.Module, prefix: str, layer_inputs: List[Tuple[tuple, dic
             gs = _group_size_for_mean(a, cols)
             rows = ops.awq_weight_mean_segments([ref.weight for ref in refs], gs, list(wsums))
             assert len(set(rows)) == 1
-            wm.copy_(wsums.to(torch.bfloat16) / rows[0])
+            wm.copy_(_div_count_bf16(wsums.to(torch.bfloat16), rows[0]))
         else:
             for k, ref in enumerate(refs):
                 am = _AbsMean(bf16=bf16)

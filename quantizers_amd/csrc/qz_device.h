@@ -56,15 +56,30 @@ __device__ __forceinline__ void st16_wt(void* p, const uint4 v) {
 // tails and whole launches were slower in the plan although faster launch by launch in isolation
 // (profiles/r05e_tune_plan.log, r05f_tune_plan.log).  The FP8_BLOCK strip kernel takes none
 // (qz_block.hip).
+// The tail is taken only by launches whose outputs are at least QZ_WT_MIN_OUT_BYTES: below that the
+// "tail" would be the whole launch (every workgroup pays the quad gather and 1 lane in 4 stores),
+// which cost the one-weight [11008, 4096] launch (22.5 MB of codes) 0.4-0.5 us in the bench's
+// pattern (12 rotating weights into 100 fresh output sets: 20.92 / 21.08 / 20.64 us with it, 20.46
+// / 20.56 / 20.44 us gated, on three boxes, rocprof medians of 700 launches; profiles/r06a-d_wt_ab.log).
+// It wins only when a launch rewrites the outputs the previous one wrote (19.56-20.16 vs 20.28-20.44
+// us), which no product path does.  Fractional tails (1/8, 1/4, 1/2 of the outputs), 4-B sc1 and
+// default-policy code stores for such launches measured no better.  Every launch of the headline
+// plan writes >= 90 MiB, so it keeps its tail (1354.1 / 1381.3 / 1390 us per step, gated vs
+// 1354.1 / 1385.0 / 1392 ungated).
 #ifndef QZ_WT_TAIL_BYTES
 #define QZ_WT_TAIL_BYTES (32ll << 20)
+#endif
+#ifndef QZ_WT_MIN_OUT_BYTES
+#define QZ_WT_MIN_OUT_BYTES (2 * QZ_WT_TAIL_BYTES)
 #endif
 __device__ __forceinline__ bool wt_tail(uint32_t wt_from) {
   return blockIdx.y * gridDim.x + blockIdx.x >= wt_from;
 }
 // first workgroup of the write-through tail of a launch of `wgs` workgroups writing `out_bytes`
+// (0xffffffff = no tail)
 inline uint32_t wt_tail_from(int64_t wgs, int64_t out_bytes, int64_t tail_bytes = QZ_WT_TAIL_BYTES) {
-  if (wgs <= 0 || out_bytes <= 0 || wgs >= 0xffffffffll) return 0xffffffffu;
+  if (out_bytes < QZ_WT_MIN_OUT_BYTES) return 0xffffffffu;
+  if (wgs <= 0 || out_bytes <= 0 || wgs >= 0xffffffffll || tail_bytes <= 0) return 0xffffffffu;
   const int64_t per = (out_bytes + wgs - 1) / wgs;
   const int64_t tail = (tail_bytes + per - 1) / per;
   return (uint32_t)(tail >= wgs ? 0 : wgs - tail);

@@ -281,10 +281,11 @@ __device__ __forceinline__ void encode_store(const FastArgs& A, const QP& p, con
       const uint32_t o_lo = __builtin_amdgcn_perm(__float_as_uint(q[1].y), __float_as_uint(q[0].y), 0x0c0c0400u);
       const uint32_t o_hi = __builtin_amdgcn_perm(__float_as_uint(q[3].y), __float_as_uint(q[2].y), 0x04000c0cu);
       const uint32_t word = ((o_lo | o_hi) << 4) | (e_lo | e_hi);
-      if (NTS && wt_tail(A.wt_from)) {
+      if (NTS && wt_tail(A.wt_from) && (reinterpret_cast<uintptr_t>(A.q_out) & 15u) == 0) {
         // the 4 words of a lane quad (4 consecutive units of one slice: 16 contiguous bytes; the
         // host sets wt only when every slice holds a multiple of 4 units, so a quad is valid as a
-        // whole) gathered into its first lane by DPP quad broadcasts, one 16-B write-through store
+        // whole) gathered into its first lane by DPP quad broadcasts, one 16-B write-through store;
+        // a codes buffer that is not 16-B aligned (a caller's table entry) keeps the 4-B stores
         const uint32_t w1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0x55, 0xF, 0xF, true);
         const uint32_t w2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xAA, 0xF, 0xF, true);
         const uint32_t w3 = (uint32_t)__builtin_amdgcn_mov_dpp((int)word, 0xFF, 0xF, 0xF, true);
@@ -1637,7 +1638,8 @@ static int quantize_impl(const void* w, int64_t batch, int64_t rows, int64_t col
     }
     const int64_t n_tiles = cdiv(F.units_per_batch, tile_unroll(fq, nt) * WAVE);
     const int64_t blocks = cdiv(n_tiles, FBLOCK / WAVE);
-    if (!fq && pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits == 4 && F.units_per_batch % 4 == 0)
+    if (!fq && pl.kind == K_INT && out_fmt == QZ_OUT_PACKED_INT32 && a->num_bits == 4 && F.units_per_batch % 4 == 0 &&
+        aligned(q_out, 16))
       F.wt_from = wt_tail_from(blocks * batch, batch * F.units_per_batch * 4);
     hipLaunchKernelGGL(pick_fast(logl, pl.kind, pl.p.sym != 0, fq, nt), dim3((unsigned)blocks, (unsigned)batch),
                        dim3(FBLOCK), 0, st, F);

@@ -17,11 +17,67 @@ def test_running_mean_bf16_matches_literal_oracle():
         prev = ct.awq_accumulate_mean_literal(x, prev)
     parts = [(x.abs().float().sum(0), x.shape[0]) for x in xs]
     got = awq._running_mean_bf16(parts)
+    # against the CPU reading (true division) and f32 batch sums in another order: within 1 ulp
     d = (got.view(torch.int16).int() - prev[0].view(torch.int16).int()).abs()
-    assert d.max() <= 1 and (d > 0).float().mean() < 0.02  # per-batch sums: f32 order vs torch's bf16 sum
-    exact = awq._running_mean_bf16([(x.abs().sum(0).float(), x.shape[0]) for x in xs])  # torch's own batch sums
-    assert torch.equal(exact.view(torch.int16), prev[0].view(torch.int16))
+    assert d.max() <= 1 and (d > 0).float().mean() < 0.02
+    # torch's own batch sums: bit for bit with the device reading (reciprocal division)
+    dev_prev = None
+    for x in xs:
+        dev_prev = ct.awq_accumulate_mean_literal(x, dev_prev, device_division=True)
+    exact = awq._running_mean_bf16([(x.abs().sum(0).float(), x.shape[0]) for x in xs])
+    assert torch.equal(exact.view(torch.int16), dev_prev[0].view(torch.int16))
     assert awq._running_mean_bf16([(torch.zeros(4), 0)]) is None
+
+
+def test_oracle_from_kernel_sums_reproduces_product():
+    """fed the statistics kernels' own sums (absmean: f32 per calibration
+    batch; w_mean: f64 per balance layer), the literal oracle's combination steps
+    (ct_torch.awq_running_mean_from_sums_literal / awq_layer_means_from_sums_literal, device
+    semantics) give the product's bf16 x_mean and w_mean bit for bit -- single operand
+    (_running_mean_bf16, _layer_means_bf16) and batched over experts (_running_means_bf16).  What
+    is left between the product and the fully literal oracle is the kernels' summation order
+    (f32 / f64 vs torch's bf16 sum) and the device powf of the grid formula."""
+    g = torch.Generator().manual_seed(11)
+    C = 512
+    for trial in range(6):
+        nb = 1 + trial * 3
+        counts = [int(v) for v in torch.randint(0, 2049, (nb,), generator=g)]
+        counts[0] = max(counts[0], 1)
+        scale = 10.0 ** torch.empty(C).uniform_(-3, 2, generator=g)
+        sums = [(torch.rand(C, generator=g) * scale * n).float() for n in counts]
+        want = ct.awq_running_mean_from_sums_literal(list(zip(sums, counts)), device_division=True)[0]
+        got = awq._running_mean_bf16(list(zip(sums, counts)))
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), trial
+        batched = awq._running_means_bf16(torch.stack(sums)[None], [counts])[0]
+        assert torch.equal(batched.view(torch.int16), want.view(torch.int16)), trial
+        rows = [int(v) for v in torch.randint(1, 20000, (1 + trial % 4,), generator=g)]
+        wsums = [(torch.rand(C, generator=g, dtype=torch.float64) * r * 0.6) for r in rows]
+        want_w = ct.awq_layer_means_from_sums_literal(list(zip(wsums, rows)), device_division=True)
+        got_w = awq._layer_means_bf16(list(zip(wsums, rows)))
+        assert got_w.dtype == torch.bfloat16
+        assert torch.equal(got_w.view(torch.int16), want_w.view(torch.int16)), trial
+
+
+def test_device_and_cpu_division_rarely_differ_on_bf16():
+    """D8's one device-dependent op, bf16 tensor / count: torch's GPU form (product with the f32
+    reciprocal) and its CPU form (true division) differ by at most 1 ulp and almost never -- an
+    8-bit dividend over an integer count lands within the reciprocal's error of a bf16 rounding
+    midpoint only for rare (mantissa, count) pairs, at every exponent of such a mantissa (243 of
+    325,120,000 (bf16, count) pairs over every positive normal bf16 and the counts 1, 8, ...,
+    69994; 241 here, where three of the eleven counts are such counts: 49351, 54503, 65535).
+    Every positive normal bf16 against these counts: the departure of the product's device form
+    from the CPU reading."""
+    import numpy as np
+    u = np.arange(0x0080, 0x7F80, dtype=np.uint32)
+    t = torch.from_numpy((u << 16).view(np.float32)).to(torch.bfloat16)
+    diff = 0
+    counts = (1, 3, 7, 100, 2047, 2048, 16383, 32768, 49351, 54503, 65535)
+    for n in counts:
+        a = ct.div_scalar_bf16(t, n, True).view(torch.int16).int()
+        b = ct.div_scalar_bf16(t, n, False).view(torch.int16).int()
+        assert (a - b).abs().max() <= 1
+        diff += int((a != b).sum())
+    assert 0 < diff < 1e-3 * t.numel() * len(counts), diff
 
 
 @pytest.mark.parametrize("duo", [True, False])
