@@ -180,7 +180,16 @@ def _event_median(fn, stream, passes=PASSES, warm=1, warm_s=WARM_S):
     return sorted(ts)[len(ts) // 2], ts
 
 
-def mixed_plan_leg(ops, dev, stream, steps=10):
+def _launch_us(gq, stream, reps=10, passes=7):
+    """One grouped launch's steady duration (us): ``reps`` launches back to back between one pair
+    of HIP events (the gaps between them included, as in a plan step), median of ``passes``."""
+    def batch():
+        for _ in range(reps):
+            gq.run(stream)
+    return _event_median(batch, stream, passes=passes, warm=1, warm_s=0.02)[0] * 1e6 / reps
+
+
+def mixed_plan_leg(ops, dev, stream, steps=20):
     """BASELINE.json configs[2] through the product: the Qwen3-4B model (public dims, random bf16)
     under the mixed recipe (configs/recipes/mixed_fp8_block_awq_int4.yaml = the reference's
     recipe_mixed_fp8_int4.yaml with quirk M1 corrected: FP8_BLOCK on q/k/v/o, int4 sym g32 on
@@ -202,7 +211,7 @@ def mixed_plan_leg(ops, dev, stream, steps=10):
     alg = plan.alg_bytes()
     per = []
     for gq, part, *_ in plan.grouped:
-        us = _event_median(lambda gq=gq: gq.run(stream), stream, passes=11, warm=2)[0] * 1e6
+        us = _launch_us(gq, stream)
         rb = sum(w.numel() * 2 for _, w in part)
         nb = rb + sum(t.numel() * t.element_size() for o in gq.outs for t in o.values() if t is not None)
         per.append({"scheme": "FP8_BLOCK 128x128" if ops.is_fp8_block128(gq.a) else
@@ -214,7 +223,7 @@ def mixed_plan_leg(ops, dev, stream, steps=10):
            "read_frac": plan.params * 2 / s / 1e9 / HBM_PEAK_GBS, "per_launch": per,
            "recipe": "configs/recipes/mixed_fp8_block_awq_int4.yaml",
            "timing": f"HIP events on the launch stream around {steps} CompressionPlan steps, median of {PASSES} "
-                     f"such passes; per launch: one event pair per launch, median of 11"}
+                     f"such passes; per launch: bench._launch_us"}
     del plan, units, model
     torch.cuda.empty_cache()
     return res
@@ -844,20 +853,13 @@ def main():
               "how": "HIP events around 100 steps after 50 more untimed ones, right after the timed region; "
                      "informational (value and roofline use the W / K given)"}
 
-    # per-launch durations (untimed, after the regions above): each launch 11 times back to back,
-    # one event pair per launch, the median (a single launch after a synchronize can catch a clock
-    # transient)
+    # per-launch durations (untimed, after the regions above): each launch 10 times back to back
+    # between one event pair, median of 7 such passes (_launch_us)
     per_launch = []
     for gq, part, *_ in plan.grouped:
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(12)]
-        evs[0].record(stream)
-        for i in range(11):
-            gq.run(stream)
-            evs[i + 1].record(stream)
-        torch.cuda.synchronize()
         nb = sum(w.numel() * 2 for _, w in part) + sum(t.numel() * t.element_size() for o in gq.outs
                                                          for t in o.values() if t is not None)
-        us = sorted(evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(11))[5]
+        us = _launch_us(gq, stream)
         rb = sum(w.numel() * 2 for _, w in part)
         per_launch.append({"shapes": sorted({f"{r}x{c}" for r, c in gq.shapes}), "weights": gq.n,
                            "us": us, "alg_bytes": nb, "read_bytes": rb,
