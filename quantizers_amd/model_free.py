@@ -7,11 +7,14 @@ Every floating 2-D ``<module>.weight`` tensor whose module name is not matched b
 is a quantization target (a checkpoint has no module types; the reference's ignore list names
 the non-Linear 2-D tensors such as ``model.embed_tokens``).  Per shard file:
 
-  disk --(reader threads, mmap)--> host --H2D (pinned staging)--> fused HIP quantize+pack (ops.compress_weights:
-       the file's same-shape weights in one grouped launch) --async D2H, pinned--> host
-       --(writer threads, after the copy event)--> disk
+  disk --(max_workers reader threads: pread of each target's bytes into pinned slots, DMA per slot;
+       staging.DiskStager)--> device --fused HIP quantize+pack (ops.compress_weights: the file's
+       same-shape weights in one grouped launch)--> --async D2H, pinned--> host
+       --(WRITE_THREADS writer threads, after the copy event)--> disk
 
-Reads of file i+1 and writes of file i-1 overlap the GPU work on file i.  Output shards keep
+The targets are chosen from each file's safetensors header alone; the other tensors (norms,
+embeddings, ignored weights) are memory-mapped and read when the output shard is written.  The
+reads of files i+1 .. i+LOOKAHEAD and the writes of earlier files overlap the GPU work on file i.  Output shards keep
 the input file names; ``model.safetensors.index.json`` and ``config.json`` (with
 ``quantization_config``) are rewritten and every other file (tokenizer, generation config) is
 copied.  Multi-GPU: under ``torch.distributed`` (one process per GPU), files are assigned to
@@ -29,6 +32,7 @@ import json
 import logging
 import os
 import shutil
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Union
 
@@ -42,11 +46,13 @@ from .compressor import _HostCopier, quantization_config_for
 from .distributed import plan_shards
 from .quantization import QuantizationArgs, QuantizationScheme, preset_scheme
 from .recipe import match_any
-from .staging import H2DStager
+from .staging import DiskStager, safetensors_header
 
 log = logging.getLogger(__name__)
 
 _FLOATS = (torch.bfloat16, torch.float16, torch.float32)
+LOOKAHEAD = 2  # files whose reads are queued ahead of the one being quantized
+WRITE_THREADS = 4  # output shards written concurrently
 
 
 def _scheme(scheme: Union[str, QuantizationScheme, dict]) -> QuantizationScheme:
@@ -87,59 +93,123 @@ def is_target(name: str, t_shape, t_dtype, ignore: List[str]) -> bool:
     return not match_any(name[: -len(".weight")], "Linear", ignore)
 
 
+# Phase record of the latest model_free_ptq call on this process (scripts/model_free_bench.py):
+# host spans (read / stage / write: perf_counter start, end, bytes) and device spans (h2d / kernel /
+# d2h: pairs of timing events, resolved to seconds when the call ends).
+LAST_RUN: Dict[str, object] = {}
+
+
+def _span(kind: str, t0: float, nbytes: int) -> None:
+    spans = LAST_RUN.setdefault("host", [])
+    spans.append((kind, t0, time.perf_counter(), nbytes))  # list.append is atomic under the GIL
+
+
 def _read(path: str) -> Dict[str, torch.Tensor]:
+    t0 = time.perf_counter()
     out = {}
     with safe_open(path, framework="pt", device="cpu") as f:
         for k in f.keys():
             out[k] = f.get_tensor(k)
+    _span("read", t0, sum(t.numel() * t.element_size() for t in out.values()))
     return out
 
 
-def _quantize_file(tensors: Dict[str, torch.Tensor], sch: QuantizationScheme, ignore: List[str], device,
-                   quantized: List[str], skipped: List[str], copier=None, stager=None) -> Dict[str, torch.Tensor]:
-    """One shard's output tensors.  Every target of the file goes to the device (through the
-    pinned staging buffers of ``stager`` when given), then ONE
-    ``ops.compress_weights`` call quantizes them (same-shape weights in one grouped launch);
-    with ``copier`` the compressed tensors come back through pinned memory asynchronously (valid
-    once the copier's last event completes)."""
+_DT_TAGS = {"BF16": torch.bfloat16, "F16": torch.float16, "F32": torch.float32}
+
+
+def _select(meta, sch: QuantizationScheme, ignore: List[str]):
+    """A file's tensors split by the header alone: (target names to quantize, their modules, D13
+    skips).  A floating 2-D target that is not bf16 raises (the kernels read bf16)."""
     a = sch.weights
-    out: Dict[str, torch.Tensor] = {}
-    mods: List[str] = []
-    ws: List[torch.Tensor] = []
-    for name in sorted(tensors):
-        t = tensors[name]
-        if not is_target(name, tuple(t.shape), t.dtype, ignore):
-            out[name] = t
+    targets, mods, skipped = [], [], []
+    for name in sorted(meta):
+        tag, shape, _ = meta[name]
+        dt = _DT_TAGS.get(tag)
+        if dt is None or not is_target(name, shape, dt, ignore):
             continue
         mod = name[: -len(".weight")]
-        if t.dtype != torch.bfloat16:
-            raise ValueError(f"{name}: weights must be bfloat16 for the GPU quantizer (got {t.dtype})")
-        if not _divisible(t.shape, a):
+        if dt != torch.bfloat16:
+            raise ValueError(f"{name}: weights must be bfloat16 for the GPU quantizer (got {dt})")
+        if not _divisible(shape, a):
             log.warning("model_free_ptq: %s %s not divisible by the scheme's groups/blocks; left unquantized (D13)",
-                        name, tuple(t.shape))
+                        name, tuple(shape))
             skipped.append(mod)
-            out[name] = t
             continue
+        targets.append(name)
         mods.append(mod)
-        ws.append(stager.copy(t) if stager is not None else t.to(device))
-    if not ws:
-        return out
-    if stager is not None:
-        stager.wait()  # the quantize launches (current stream) see the staged weights
-    comps = ops.compress_weights(ws, a, has_activation_quant=sch.input_activations is not None)
-    dev_out = {f"{mod}.{k}": v for mod, comp in zip(mods, comps) for k, v in comp.items()}
-    if copier is not None:
-        out.update(copier.submit(dev_out))
-    else:
-        out.update({k: (v.to("cpu") if v.is_cuda else v) for k, v in dev_out.items()})
-    quantized.extend(mods)
+    return targets, mods, skipped
+
+
+def _rest(path: str, meta, targets: List[str]) -> Dict[str, torch.Tensor]:
+    """The file's other tensors (norms, embeddings, ignored or skipped weights), unchanged: memory-
+    mapped host tensors, read when the output shard is written."""
+    keep = set(targets)
+    out = {}
+    with safe_open(path, framework="pt", device="cpu") as f:
+        for k in meta:
+            if k not in keep:
+                out[k] = f.get_tensor(k)
     return out
+
+
+def _quantize_file(ws: List[torch.Tensor], mods: List[str], sch: QuantizationScheme, device, copier=None
+                   ) -> Dict[str, torch.Tensor]:
+    """One shard's compressed tensors: ONE ``ops.compress_weights`` call over the file's device-
+    resident targets (same-shape weights in one grouped launch); with ``copier`` they come back
+    through pinned memory asynchronously (valid once the copier's last event completes)."""
+    if not ws:
+        return {}
+    in_bytes = sum(w.numel() * 2 for w in ws)
+    kern = _dev_pair(torch.cuda.current_stream(device))
+    comps = ops.compress_weights(ws, sch.weights, has_activation_quant=sch.input_activations is not None)
+    kern[1].record(torch.cuda.current_stream(device))
+    dev_out = {f"{mod}.{k}": v for mod, comp in zip(mods, comps) for k, v in comp.items()}
+    out_bytes = sum(v.numel() * v.element_size() for v in dev_out.values() if v.is_cuda)
+    LAST_RUN.setdefault("dev", []).append(("kernel", kern, in_bytes + out_bytes))
+    if copier is None:
+        return {k: (v.to("cpu") if v.is_cuda else v) for k, v in dev_out.items()}
+    d2h = _dev_pair(copier.stream, after=torch.cuda.current_stream(device))
+    out = copier.submit(dev_out)
+    d2h[1].record(copier.stream)
+    LAST_RUN.setdefault("dev", []).append(("d2h", d2h, out_bytes))
+    return out
+
+
+def _dev_pair(stream, after=None):
+    """A (start, end) pair of timing events; start recorded now on ``stream`` (behind ``after``'s
+    work so far when given), end recorded by the caller."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if after is not None:
+        stream.wait_stream(after)
+    e0.record(stream)
+    return e0, e1
 
 
 def _write_shard(out: Dict[str, torch.Tensor], path: str, ready) -> None:
     if ready is not None:
         ready.synchronize()  # the shard's device->host copies have landed
+    t0 = time.perf_counter()
     save_file({k: v.contiguous() for k, v in out.items()}, path, {"format": "pt"})
+    _span("write", t0, os.path.getsize(path))
+
+
+def run_summary() -> Dict[str, Dict[str, float]]:
+    """Per phase of the latest call: busy seconds (the sum of its spans), bytes, GB/s while busy;
+    ``wall`` = the call's wall seconds.  Device phases are resolved from their events (the call
+    has synchronised)."""
+    res: Dict[str, Dict[str, float]] = {}
+    for kind, t0, t1, nb in LAST_RUN.get("host", []):
+        r = res.setdefault(kind, {"s": 0.0, "bytes": 0})
+        r["s"] += t1 - t0
+        r["bytes"] += nb
+    for kind, (e0, e1), nb in LAST_RUN.get("dev", []):
+        r = res.setdefault(kind, {"s": 0.0, "bytes": 0})
+        r["s"] += e0.elapsed_time(e1) * 1e-3
+        r["bytes"] += nb
+    for r in res.values():
+        r["GBps"] = r["bytes"] / r["s"] / 1e9 if r["s"] else 0.0
+    res["wall"] = {"s": LAST_RUN.get("wall", 0.0)}
+    return res
 
 
 def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, QuantizationScheme, dict] = "FP8_BLOCK",
@@ -153,6 +223,8 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
         raise ValueError("scheme has no weight quantization")
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
+    LAST_RUN.clear()
+    t_call = time.perf_counter()
     if device is None:
         device = torch.device("cuda", torch.cuda.current_device())
     device = torch.device(device)
@@ -169,25 +241,45 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
     skipped: List[str] = []
     weight_map: Dict[str, str] = {}
     total = 0
-    with ThreadPoolExecutor(max_workers=max(2, max_workers)) as pool:
-        reads = [pool.submit(_read, os.path.join(model_stub, f)) for f in mine[:2]]
-        writes = []
+    with ThreadPoolExecutor(max_workers=max(2, max_workers)) as pool, \
+            ThreadPoolExecutor(max_workers=WRITE_THREADS) as wpool:
+        stager = DiskStager(device, pool)
         copier = _HostCopier(device)
-        stager = H2DStager(device)
+
+        def enqueue(fn):  # header, target selection, and the file's reads + DMAs queued on the pool
+            path = os.path.join(model_stub, fn)
+            hdr = safetensors_header(path)
+            targets, mods, sk = _select(hdr[1], sch, ignore)
+            return path, hdr, targets, mods, sk, stager.load(path, targets, hdr)
+
+        pending = [enqueue(f) for f in mine[:LOOKAHEAD]]
+        writes = []
         for i, fn in enumerate(mine):
-            tensors = reads[i].result()
-            if i + 2 < len(mine):
-                reads.append(pool.submit(_read, os.path.join(model_stub, mine[i + 2])))
-            out = _quantize_file(tensors, sch, ignore, device, quantized, skipped, copier, stager)
+            path, hdr, targets, mods, sk, fl = pending[i]
+            pending[i] = None
+            if i + LOOKAHEAD < len(mine):
+                pending.append(enqueue(mine[i + LOOKAHEAD]))
+            t_wait = time.perf_counter()
+            h2d = _dev_pair(stager.stream)
+            dev = stager.wait(fl)  # the quantize launches (current stream) see the loaded weights
+            h2d[1].record(stager.stream)
+            LAST_RUN.setdefault("dev", []).append(("h2d", h2d, fl.nbytes))
+            _span("read_wait", t_wait, fl.nbytes)  # the main thread blocked on this file's reads
+            out = _rest(path, hdr[1], targets)
+            out.update(_quantize_file([dev[n] for n in targets], mods, sch, device, copier))
+            del dev, fl
+            quantized.extend(mods)
+            skipped.extend(sk)
             ready = copier.last_event
             for k, t in out.items():
                 weight_map[k] = fn
                 total += t.numel() * t.element_size()
-            writes.append(pool.submit(_write_shard, out, os.path.join(save_directory, fn), ready))
-            reads[i] = None
+            writes.append(wpool.submit(_write_shard, out, os.path.join(save_directory, fn), ready))
         for w in writes:
             w.result()
         copier.finish()
+    torch.cuda.synchronize(device)
+    LAST_RUN["wall"] = time.perf_counter() - t_call
     state = (weight_map, total, quantized, skipped)
     if world > 1:
         allst = [None] * world
