@@ -1,13 +1,13 @@
 """Prototype A/B: the fused GEMM -> grid loss kernel (quantizers_amd/csrc/proto/
-qz_gemm_loss.hip, built into csrc/proto/libqz_proto.so) against the product's per-grid-point path
-(torch's bf16 linear = hipBLASLt, then ops.awq_sq_err_accum) on the Qwen3-30B-A3B expert w2 problem:
-X [32768, 768] x W [2048, 768]^T, loss against R [32768, 2048].
+qz_gemm_loss.hip, built into csrc/proto/libqz_proto.so) against the product's expert-search path
+(awq._batched_losses: torch's bf16 mm = hipBLASLt per grid point, MULTI_LOSS = 8 outputs per
+ops.awq_sq_err_partials_multi launch, one ordered reduce) on the Qwen3-30B-A3B expert w2 problem:
+X [32768, 768] x W [2048, 768]^T, losses against R [32768, 2048].
 
-1. layout check with exact small-integer data (every product exact in f32): C must equal torch's;
-2. random data: C vs torch's (fraction of bf16 outputs that differ; GEMM rounding order only);
-3. timing (HIP events, median of 7 passes of 20 launches): hipBLASLt GEMM, loss kernel, the two
-   together (the product's per-grid-point cost), the prototype's GEMM core (bf16 store) and its
-   fused loss mode; PFLOP/s of each GEMM; the fused loss vs the reference loss.
+1. layout check with exact small-integer data (every product exact in f32), both orientations;
+2. losses on random data, single items, ragged rows and a batch of 8 grid points, vs the product's;
+3. timing (HIP events, median of 7 passes): per grid point, the product's path and the fused
+   launch (one item, and 8 grid points x E experts per launch).
 """
 import ctypes
 import os
@@ -25,61 +25,73 @@ I64 = ctypes.c_int64
 
 def main():
     lib = ctypes.CDLL(os.environ.get("PROTO_LIB", os.path.join(ROOT, "quantizers_amd/csrc/proto/libqz_proto.so")))
-    lib.qzp_gemm_nt.argtypes = [P, P, P, P, P, I64, I64, I64, I64, I64, I64, ctypes.c_int, P]
+    lib.qzp_gemm_sqerr.argtypes = [P, I64, I64, I64, I64, P, ctypes.c_int, P]
+    lib.qzp_gemm_sqerr_tiles.argtypes = [I64, I64]
+    lib.qzp_gemm_sqerr_tiles.restype = I64
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream()
     T, N, K = int(os.environ.get("T", 32768)), int(os.environ.get("N", 2048)), int(os.environ.get("K", 768))
     g = torch.Generator(device=dev).manual_seed(0)
 
-    def run(x, w, r, c, part, mode):
-        rc = lib.qzp_gemm_nt(P(x.data_ptr()), P(w.data_ptr()), P(r.data_ptr()), P(c.data_ptr()), P(part.data_ptr()),
-                             T, N, K, x.stride(0), w.stride(0), r.stride(0), mode, P(st.cuda_stream))
+    def table(items, nb):
+        """items: [(x, w, r, rows)] -> (device table, part [n, nb])"""
+        part = torch.zeros(len(items), nb, dtype=torch.float64, device=dev)
+        rows = [[x.data_ptr(), w.data_ptr(), r.data_ptr(), part[i].data_ptr(), nr] for i, (x, w, r, nr) in enumerate(items)]
+        return torch.tensor(rows, dtype=torch.int64, device=dev), part
+
+    def launch(tab, n, rows_max, c, mode):
+        rc = lib.qzp_gemm_sqerr(P(tab.data_ptr()), n, rows_max, N, K, P(c.data_ptr() if c is not None else 0), mode,
+                                P(st.cuda_stream))
         assert rc == 0, rc
 
-    nparts = (T // 256) * (N // 256)
-    part = torch.zeros(nparts, dtype=torch.float64, device=dev)
-    # 1. exact layout check, both MFMA shapes
+    nb = lib.qzp_gemm_sqerr_tiles(T, N)
+    # 1. exact layout check, both orientations
     xi = torch.randint(-3, 4, (T, K), device=dev, generator=g).to(torch.bfloat16)
     wi = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(torch.bfloat16)
     ci = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
     ref = (xi.float() @ wi.float().t()).to(torch.bfloat16)
-    for mode in (0, 2, 8, 10):
+    for mode in (0, 2, 4, 6, 8):
         ci.zero_()
-        run(xi, wi, ci, ci, part, mode)
+        tab, _ = table([(xi, wi, ci, T)], nb)
+        launch(tab, 1, T, ci, mode)
         exact = torch.equal(ci.view(torch.int16), ref.view(torch.int16))
         print(f"layout check mode {mode} (exact integer data): {'OK' if exact else 'MISMATCH'}", flush=True)
         if not exact:
-            bad = (ci.float() != ref.float()).nonzero()[:5].tolist()
-            print("first mismatches", bad, flush=True)
+            print("first mismatches", (ci.float() != ref.float()).nonzero()[:5].tolist(), flush=True)
             return
     del xi, wi, ci, ref
-    # 2. random data
-    x = (torch.randn(T, K, device=dev, generator=g)).to(torch.bfloat16)
+    # 2. losses
+    x = torch.randn(T, K, device=dev, generator=g).to(torch.bfloat16)
     w = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(torch.bfloat16)
-    w2 = (w.float() + torch.randn(N, K, device=dev, generator=g) * 0.002).to(torch.bfloat16)  # "grid point"
     r = torch.nn.functional.linear(x, w)
-    c = torch.empty_like(r)
-    c_bl = torch.nn.functional.linear(x, w2)
-    loss_ref = torch.zeros(1, dtype=torch.float64, device=dev)
-    ops.awq_sq_err_accum(c_bl, r, loss_ref)
-    for mode in (0, 2, 8, 10):
-        run(x, w2, r, c, part, mode)
-        diff = (c.view(torch.int16) != c_bl.view(torch.int16)).float().mean().item()
-        rel = ((c.float() - c_bl.float()).abs().max() / c_bl.float().abs().max()).item()
-        print(f"random data mode {mode}: {diff * 100:.3f} % of bf16 outputs differ from hipBLASLt's (max rel {rel:.2e})",
-              flush=True)
-        run(x, w2, r, c, part, mode | 1)
-        torch.cuda.synchronize()
-        lf, lr = part.sum().item(), loss_ref.item()
-        print(f"loss mode {mode | 1}: fused {lf:.9e}  hipBLASLt+k_sqdiff {lr:.9e}  rel diff {(lf - lr) / lr:.2e}",
-              flush=True)
-    # 3. timing
-    flop = 2 * T * N * K
-    out = torch.empty_like(r)
-    lsum = torch.zeros(1, dtype=torch.float64, device=dev)
+    ws = [(w.float() + torch.randn(N, K, device=dev, generator=g) * 0.002 * (1 + i)).to(torch.bfloat16)
+          for i in range(8)]
 
-    def t_of(fn, n=20, passes=7):
-        for _ in range(3):
+    def ref_loss(x_, w_, r_):
+        acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        ops.awq_sq_err_accum(torch.nn.functional.linear(x_, w_), r_.contiguous(), acc)
+        return acc.item()
+    for mode in (3, 7, 9):
+        tab, part = table([(x, ws[0], r, T)], nb)
+        launch(tab, 1, T, None, mode)
+        torch.cuda.synchronize()
+        lf, lr = part.sum().item(), ref_loss(x, ws[0], r)
+        print(f"loss mode {mode}: fused {lf:.9e} product {lr:.9e} rel {(lf - lr) / lr:.2e}", flush=True)
+        for tr in (1000, 4097, 300):  # ragged rows
+            tab, part = table([(x, ws[1], r, tr)], nb)
+            launch(tab, 1, T, None, mode)
+            torch.cuda.synchronize()
+            lf, lr = part.sum().item(), ref_loss(x[:tr], ws[1], r[:tr])
+            print(f"  ragged rows {tr}: fused {lf:.9e} product {lr:.9e} rel {(lf - lr) / lr:.2e}", flush=True)
+        tab, part = table([(x, wq, r, T) for wq in ws], nb)
+        launch(tab, 8, T, None, mode)
+        torch.cuda.synchronize()
+        rel = max(abs(part[i].sum().item() / ref_loss(x, ws[i], r) - 1) for i in range(8))
+        print(f"  batch of 8 grid points: max rel {rel:.2e}", flush=True)
+
+    # 3. timing per grid point
+    def t_of(fn, per, n=5, passes=7):
+        for _ in range(2):
             fn()
         torch.cuda.synchronize()
         ts = []
@@ -90,22 +102,40 @@ def main():
                 fn()
             e1.record(st)
             torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1) * 1e3 / n)
+            ts.append(e0.elapsed_time(e1) * 1e3 / n / per)
         return sorted(ts)[len(ts) // 2]
-    legs = [
-        ("hipBLASLt linear", lambda: torch.mm(x, w2.t(), out=out), True),
-        ("k_sqdiff loss", lambda: ops.awq_sq_err_accum(out, r, lsum), False),
-        ("hipBLASLt + k_sqdiff", lambda: (torch.mm(x, w2.t(), out=out), ops.awq_sq_err_accum(out, r, lsum)), False),
-    ]
-    for mode, name in ((0, "16x16x32"), (4, "16x16x32 prio"), (2, "32x32x16"), (6, "32x32x16 prio"),
-                       (8, "pipe 16x16x32"), (10, "pipe 32x32x16")):
-        legs.append((f"proto core {name}", lambda mode=mode: run(x, w2, r, c, part, mode), True))
-        legs.append((f"proto fused {name}", lambda mode=mode: run(x, w2, r, c, part, mode | 1), False))
-    for name, fn, gemm in legs:
-        us = t_of(fn)
-        extra = f"  {flop / (us * 1e-6) / 1e15:.3f} PFLOP/s" if gemm else ""
-        print(f"{name:32s} {us:9.2f} us{extra}", flush=True)
+    E = int(os.environ.get("E", 4))
+    xs = [torch.randn(T, K, device=dev, generator=g).to(torch.bfloat16) for _ in range(E)]
+    rs = [torch.nn.functional.linear(xe, w) for xe in xs]
+    wq_all = torch.stack([torch.stack([wq] * E) for wq in ws])  # [8, E, N, K]
+    outs = [torch.empty_like(rs[0]) for _ in range(8)]
+    npart = ops.awq_sq_err_partials_count(rs[0].shape)
+    ppart = torch.empty(E, 8, npart, dtype=torch.float64, device=dev)
+    tot = torch.zeros(E * 8, dtype=torch.float64, device=dev)
 
+    def product():  # awq._batched_losses with MULTI_LOSS = 8
+        for k in range(E):
+            for j in range(8):
+                torch.mm(xs[k], wq_all[j, k].t(), out=outs[j])
+            ops.awq_sq_err_partials_multi(rs[k], outs, ppart[k])
+        ops.awq_sq_err_reduce(ppart.view(E * 8, npart), npart, tot)
+    flop = 2 * T * N * K
+    us = t_of(product, 8 * E)
+    print(f"{'product (mm + multi-loss + reduce)':40s} {us:9.2f} us per grid point", flush=True)
+    us_mm = t_of(lambda: torch.mm(xs[0], ws[0].t(), out=outs[0]), 1)
+    print(f"{'  of which hipBLASLt mm':40s} {us_mm:9.2f} us  {flop / (us_mm * 1e-6) / 1e15:.3f} PFLOP/s", flush=True)
+    cbuf = torch.empty_like(rs[0])
+    for mode in (2, 6, 8, 3, 7, 9):
+        tab1, _ = table([(xs[0], ws[0], rs[0] if mode & 1 else cbuf, T)], nb)
+        us1 = t_of(lambda: launch(tab1, 1, T, cbuf, mode), 1)
+        line = f"mode {mode} ({'fused loss' if mode & 1 else 'core, bf16 store'}, BK {64 if mode & 12 else 32}" \
+               f"{', 4 waves' if mode & 8 else ''}): one item " \
+               f"{us1:9.2f} us ({flop / (us1 * 1e-6) / 1e15:.3f} PFLOP/s)"
+        if mode & 1:
+            tabn, partn = table([(xs[k], wq_all[j, k], rs[k], T) for k in range(E) for j in range(8)], nb)
+            usn = t_of(lambda: launch(tabn, 8 * E, T, None, mode), 8 * E)
+            line += f", {8 * E} items per launch {usn:9.2f} us per grid point ({flop / (usn * 1e-6) / 1e15:.3f} PFLOP/s)"
+        print(line, flush=True)
 
 if __name__ == "__main__":
     main()
