@@ -83,7 +83,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=None,
                    help="ranks (one per GPU); without a torchrun environment bench.py starts them itself")
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    # 50 untimed steps (70 ms): the clocks settle about 25 steps (35 ms) into a load
+    # (scripts/step_ramp.py, profiles/r05j_step_ramp.log), so the K timed steps are steady state
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--copies", type=int, default=12)
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--launch-check", action="store_true",
@@ -835,9 +837,9 @@ def main():
     if args.profile_only:
         return
 
-    # steady state of the same plan (informational, never `value`): the clocks settle about 25
-    # steps (35 ms) after the load starts (scripts/step_ramp.py, profiles/r05j_step_ramp.log), so
-    # a short K = 20 window after W = 5 includes part of that ramp
+    # steady state of the same plan (informational, never `value`): 100 steps after 50 more; equal
+    # to the timed region at the default W = 50 (the clocks settle about 25 steps into a load,
+    # profiles/r05j_step_ramp.log); a short W's timed region reads slower than it
     for _ in range(50):
         plan.run(stream)
     s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
