@@ -413,6 +413,130 @@ void k_gemm_sqerr4w(const Item* __restrict__ items, uint16_t* __restrict__ C, in
     if (tid == 0) it.part[idx] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
   }
 }
+
+// 4-wave software-pipelined variant: the fragments of the next k-substep are read (16 ds_read_b128)
+// while the 64 MFMAs of the current one issue, interleaved 1 : 4 by sched_group_barrier; two
+// fragment register sets; one barrier per 64-deep step, after which the glds for step s + 2 go into
+// the stage just drained.
+struct Frag16 {
+  bf16x8 x[8], w[8];
+};
+__device__ __forceinline__ void load_frags(Frag16& f, const uint8_t* st, int wm, int wn, int ks, int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f.w[j] = frag64(st + 32768, wn * 128 + j * 16 + (lane & 15), ks * 4 + (lane >> 4));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f.x[i] = frag64(st, wm * 128 + i * 16 + (lane & 15), ks * 4 + (lane >> 4));
+}
+__device__ __forceinline__ void mma_all(f32x4 (&acc)[8][8], const Frag16& f) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.w[j], f.x[i], acc[i][j], 0, 0, 0);
+}
+__device__ __forceinline__ void interleave_16r_64m() {
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMA
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_gemm_sqerr4p(const Item* __restrict__ items, uint16_t* __restrict__ C, int64_t N, int64_t K, int64_t tiles_max) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const Item it = items[blockIdx.y];
+  const int ntn = (int)(N / BN);
+  const int64_t tiles = (it.rows + BM - 1) / BM * ntn;
+  const int64_t b = blockIdx.x, xcd = b & 7, q8 = tiles_max >> 3, r8 = tiles_max & 7;
+  const int64_t idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  if (idx >= tiles) {
+    if (MODE == 1 && tid == 0) it.part[idx] = 0.0;
+    return;
+  }
+  const int64_t t0 = idx / ntn * BM, n0 = idx % ntn * BN;
+  constexpr int BK2 = 64, ST2 = 65536, ST2A = 32768;
+  const int nk2 = (int)(K / BK2);
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint16_t* gx[8];
+  const uint16_t* gw[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int row = w * 64 + q * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((row >> 1) & 7);
+    const int64_t rx = t0 + row < it.rows ? t0 + row : it.rows - 1;
+    gx[q] = it.x + rx * K + c * 8;
+    gw[q] = it.w + (n0 + row) * K + c * 8;
+  }
+  auto stage64 = [&](int s, uint8_t* dst) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      __builtin_amdgcn_global_load_lds((const void*)(gx[q] + s * BK2),
+                                       (__attribute__((address_space(3))) void*)(dst + (w * 8 + q) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(gw[q] + s * BK2),
+                                       (__attribute__((address_space(3))) void*)(dst + ST2A + (w * 8 + q) * 1024), 16,
+                                       0, 0);
+    }
+  };
+  Frag16 f0, f1;
+  stage64(0, lds);
+  if (nk2 > 1) stage64(1, lds + ST2);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // step 0 (this wave's 16 loads) landed
+  __builtin_amdgcn_s_barrier();
+  load_frags(f0, lds, wm, wn, 0, lane);
+  for (int s = 0; s < nk2; ++s) {
+    const uint8_t* st = lds + (s & 1) * ST2;
+    // half 1: read (s, ks 1) while the MFMAs of (s, ks 0) issue
+    load_frags(f1, st, wm, wn, 1, lane);
+    mma_all(acc, f0);
+    interleave_16r_64m();
+    // every wave has read stage s; step s + 1 landed: barrier, then refill stage s with step s + 2
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (s + 2 < nk2) stage64(s + 2, lds + (s & 1) * ST2);
+    // half 2: read (s + 1, ks 0) while the MFMAs of (s, ks 1) issue
+    if (s + 1 < nk2) load_frags(f0, lds + ((s + 1) & 1) * ST2, wm, wn, 0, lane);
+    mma_all(acc, f1);
+    interleave_16r_64m();
+  }
+  double dsum = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t t = t0 + wm * 128 + i * 16 + (lane & 15);
+      const int64_t n = n0 + wn * 128 + j * 16 + (lane >> 4) * 4;
+      const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+      if (t >= it.rows) continue;
+      if constexpr (MODE == 0) {
+        *reinterpret_cast<uint2*>(C + t * N + n) = make_uint2(lo, hi);
+      } else {
+        const uint2 rv = *reinterpret_cast<const uint2*>(it.r + t * N + n);
+        const float d0 = bf2f(f2bf(bf2f(lo & 0xffffu) - bf2f(rv.x & 0xffffu)));
+        const float d1 = bf2f(f2bf(bf2f(lo >> 16) - bf2f(rv.x >> 16)));
+        const float d2 = bf2f(f2bf(bf2f(hi & 0xffffu) - bf2f(rv.y & 0xffffu)));
+        const float d3 = bf2f(f2bf(bf2f(hi >> 16) - bf2f(rv.y >> 16)));
+        dsum += (double)(d0 * d0 + d1 * d1) + (double)(d2 * d2 + d3 * d3);
+      }
+    }
+  if constexpr (MODE == 1) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dsum += __shfl_xor(dsum, off);
+    double* wsum = reinterpret_cast<double*>(lds);
+    __syncthreads();
+    if (lane == 0) wsum[w] = dsum;
+    __syncthreads();
+    if (tid == 0) it.part[idx] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+  }
+}
 }  // namespace
 
 // items: device array of n Item rows {x, w, r, part, rows}; every item N x K (dense rows: ld = K for
@@ -430,6 +554,12 @@ extern "C" int qzp_gemm_sqerr(const void* items, int64_t n, int64_t rows_max, in
                              k_gemm_sqerr<1, true>,    k_gemm_sqerr64<0, false>, k_gemm_sqerr64<1, false>,
                              k_gemm_sqerr64<0, true>,  k_gemm_sqerr64<1, true>};
   if ((mode & 4) && K % 64) return -1;
+  if (mode & 16) {  // the 4-wave software-pipelined variant (BK 64)
+    if (K % 64) return -1;
+    hipLaunchKernelGGL((mode & 1) ? k_gemm_sqerr4p<1> : k_gemm_sqerr4p<0>, dim3((unsigned)tiles_max, (unsigned)n),
+                       dim3(256), 0, (hipStream_t)stream, (const Item*)items, (uint16_t*)C, N, K, tiles_max);
+    return (int)hipGetLastError();
+  }
   if (mode & 8) {  // the 4-wave variant (BK 64)
     if (K % 64) return -1;
     hipLaunchKernelGGL((mode & 1) ? k_gemm_sqerr4w<1> : k_gemm_sqerr4w<0>, dim3((unsigned)tiles_max, (unsigned)n),

@@ -50,7 +50,7 @@ def main():
     wi = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(torch.bfloat16)
     ci = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
     ref = (xi.float() @ wi.float().t()).to(torch.bfloat16)
-    for mode in (0, 2, 4, 6, 8):
+    for mode in (0, 2, 4, 6, 8, 16):
         ci.zero_()
         tab, _ = table([(xi, wi, ci, T)], nb)
         launch(tab, 1, T, ci, mode)
@@ -71,7 +71,7 @@ def main():
         acc = torch.zeros(1, dtype=torch.float64, device=dev)
         ops.awq_sq_err_accum(torch.nn.functional.linear(x_, w_), r_.contiguous(), acc)
         return acc.item()
-    for mode in (3, 7, 9):
+    for mode in (7, 17):
         tab, part = table([(x, ws[0], r, T)], nb)
         launch(tab, 1, T, None, mode)
         torch.cuda.synchronize()
@@ -125,11 +125,11 @@ def main():
     us_mm = t_of(lambda: torch.mm(xs[0], ws[0].t(), out=outs[0]), 1)
     print(f"{'  of which hipBLASLt mm':40s} {us_mm:9.2f} us  {flop / (us_mm * 1e-6) / 1e15:.3f} PFLOP/s", flush=True)
     cbuf = torch.empty_like(rs[0])
-    for mode in (2, 6, 8, 3, 7, 9):
+    for mode in (6, 16, 7, 17):
         tab1, _ = table([(xs[0], ws[0], rs[0] if mode & 1 else cbuf, T)], nb)
         us1 = t_of(lambda: launch(tab1, 1, T, cbuf, mode), 1)
-        line = f"mode {mode} ({'fused loss' if mode & 1 else 'core, bf16 store'}, BK {64 if mode & 12 else 32}" \
-               f"{', 4 waves' if mode & 8 else ''}): one item " \
+        line = f"mode {mode} ({'fused loss' if mode & 1 else 'core, bf16 store'}, BK {64 if mode & 28 else 32}" \
+               f"{', 4 waves' if mode & 8 else ''}{', 4 waves pipelined' if mode & 16 else ''}): one item " \
                f"{us1:9.2f} us ({flop / (us1 * 1e-6) / 1e15:.3f} PFLOP/s)"
         if mode & 1:
             tabn, partn = table([(xs[k], wq_all[j, k], rs[k], T) for k in range(E) for j in range(8)], nb)
