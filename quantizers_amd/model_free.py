@@ -94,8 +94,8 @@ def is_target(name: str, t_shape, t_dtype, ignore: List[str]) -> bool:
 
 
 # Phase record of the latest model_free_ptq call on this process (scripts/model_free_bench.py):
-# host spans (read / stage / write: perf_counter start, end, bytes) and device spans (h2d / kernel /
-# d2h: pairs of timing events, resolved to seconds when the call ends).
+# host spans (read_wait / write: perf_counter start, end, bytes) and device spans (kernel / d2h:
+# pairs of timing events, resolved to seconds when the call ends).
 LAST_RUN: Dict[str, object] = {}
 
 
@@ -260,11 +260,8 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
             if i + LOOKAHEAD < len(mine):
                 pending.append(enqueue(mine[i + LOOKAHEAD]))
             t_wait = time.perf_counter()
-            h2d = _dev_pair(stager.stream)
             dev = stager.wait(fl)  # the quantize launches (current stream) see the loaded weights
-            h2d[1].record(stager.stream)
-            LAST_RUN.setdefault("dev", []).append(("h2d", h2d, fl.nbytes))
-            _span("read_wait", t_wait, fl.nbytes)  # the main thread blocked on this file's reads
+            _span("read_wait", t_wait, fl.nbytes)  # the main thread blocked on this file's reads + DMAs
             out = _rest(path, hdr[1], targets)
             out.update(_quantize_file([dev[n] for n in targets], mods, sch, device, copier))
             del dev, fl

@@ -130,6 +130,11 @@ class DiskStager:
     def load(self, path: str, names: List[str], header=None) -> FileLoad:
         """Enqueue the reads + DMAs of ``names`` from the file at ``path``; returns at once."""
         start, meta = header if header is not None else safetensors_header(path)
+        for name in names:  # every entry checked before any read is queued
+            tag, shape, (b0, b1) = meta[name]
+            need = torch.Size(shape).numel() * torch.empty(0, dtype=_ST_DTYPES[tag]).element_size()
+            if need != b1 - b0:
+                raise ValueError(f"{path}: {name} holds {b1 - b0} bytes, its shape {shape} needs {need}")
         fd = os.open(path, os.O_RDONLY)
         tensors, futures, total = {}, [], 0
         # the blocks allocated below may have been freed by the caller's stream while its kernels
@@ -141,9 +146,6 @@ class DiskStager:
             dst.record_stream(self.stream)  # not reused by the allocator before its DMAs have run
             tensors[name] = dst
             flat = dst.reshape(-1).view(torch.uint8)
-            if flat.numel() != b1 - b0:
-                os.close(fd)
-                raise ValueError(f"{path}: {name} holds {b1 - b0} bytes, its shape {shape} needs {flat.numel()}")
             for off in range(0, b1 - b0, self.slot_bytes):
                 n = min(self.slot_bytes, b1 - b0 - off)
                 futures.append(self.pool.submit(self._chunk, fd, start + b0 + off, flat[off:off + n]))
