@@ -1,0 +1,76 @@
+"""Outside code pins the oracle's integer qparam formulas (oracle/ct_torch.calculate_qparams,
+fake_quantize): torch's own quantization observers (torch.ao.quantization.observer
+.PerChannelMinMaxObserver / MinMaxObserver, shipped in the image's torch, not written here) compute
+the same range-with-zero, symmetric divisor (qmax - qmin) / 2, asymmetric scale (max - min) /
+(qmax - qmin) and zero point qmin - round(min / scale), clamped.  Evaluated in f32 (torch.ao's
+arithmetic), the oracle's scales and zero points equal torch.ao's bit for bit, for int4 / int8,
+symmetric / asymmetric, group / channel / tensor strategies.
+
+torch.fake_quantize_per_channel_affine rounds x * (1 / scale) and then adds the zero point;
+compressed-tensors (and the oracle, and the kernels) round x / scale + zero point: the fake-quantized
+values agree except where those two forms round to different integers, and the test checks that
+is the only difference.
+
+Not pinned here: the bf16 evaluation points (D3), zero groups (D1 / D10: torch.ao clamps the scale
+to eps BEFORE the zero point, compressed-tensors >= 0.12 after it, so an all-zero asymmetric group
+gets zero point qmin there and 0 here), the FP8 / FP4 schemes."""
+import pytest
+import torch
+
+import ct_torch as ct
+from torch.ao.quantization.observer import MinMaxObserver, PerChannelMinMaxObserver
+
+
+def _weights(seed=0, rows=192, cols=1024):
+    g = torch.Generator().manual_seed(seed)
+    w = torch.randn(rows, cols, generator=g) * (torch.rand(rows, 1, generator=g) * 0.1 + 1e-3)
+    w[3] = w[3].abs()  # all-positive rows / groups: the range must still include zero
+    w[5] = -w[5].abs()
+    return w
+
+
+def _ao(x2d, sym, qmin, qmax, per_channel=True):
+    if per_channel:
+        obs = PerChannelMinMaxObserver(ch_axis=0, dtype=torch.qint8, quant_min=qmin, quant_max=qmax,
+                                       qscheme=torch.per_channel_symmetric if sym else torch.per_channel_affine)
+    else:
+        obs = MinMaxObserver(dtype=torch.qint8, quant_min=qmin, quant_max=qmax,
+                             qscheme=torch.per_tensor_symmetric if sym else torch.per_tensor_affine)
+    obs(x2d)
+    return obs.calculate_qparams()
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("sym", [True, False])
+@pytest.mark.parametrize("strategy", ["group", "channel", "tensor"])
+def test_qparams_match_torch_ao_observers(bits, sym, strategy):
+    w = _weights(seed=bits * 10 + sym)
+    a = ct.QArgs(num_bits=bits, type="int", symmetric=sym, strategy=strategy, group_size=128)
+    qmin, qmax = (int(v) for v in ct.calculate_range(a))
+    mn, mx = ct.observe_minmax(w, a)
+    s_ct, z_ct = ct.calculate_qparams(mn, mx, a)
+    # the same units as torch.ao channels: one row per group / channel, the tensor as one
+    x2d = {"group": w.reshape(-1, 128), "channel": w, "tensor": w}[strategy]
+    s_ao, z_ao = _ao(x2d, sym, qmin, qmax, per_channel=strategy != "tensor")
+    assert s_ct.dtype == torch.float32
+    assert torch.equal(s_ct.reshape(-1), s_ao.reshape(-1)), "scales"
+    assert torch.equal(z_ct.reshape(-1).long(), z_ao.reshape(-1).long()), "zero points"
+    # fake quantization: torch's kernel rounds x * (1 / s), the oracle x / s
+    fq_ct = ct.fake_quantize(w, s_ct, z_ct, a)
+    sv = s_ao.reshape(-1).float()
+    zv = z_ao.reshape(-1).int()
+    if strategy == "tensor":
+        fq_ao = torch.fake_quantize_per_tensor_affine(w, float(sv[0]), int(zv[0]), qmin, qmax)
+        s_el, z_el = sv[0], zv[0].float()
+        x = w
+    else:
+        fq_ao = torch.fake_quantize_per_channel_affine(x2d, sv, zv, 0, qmin, qmax).reshape(w.shape)
+        s_el, z_el = sv[:, None], zv[:, None].float()
+        x = x2d
+    # compressed-tensors: round(x / s + zp); torch's kernel: round(x * (1 / s)) + zp
+    q_div = torch.clamp(torch.round(x / s_el + z_el), qmin, qmax).reshape(w.shape)
+    q_mul = torch.clamp(torch.round(x * (1.0 / s_el)) + z_el, qmin, qmax).reshape(w.shape)
+    same = q_div == q_mul
+    assert torch.equal(fq_ct[same], fq_ao[same])
+    assert (~same).float().mean() < 2e-3  # the quotient forms disagree only next to a rounding tie
+    assert ((q_div - q_mul).abs() <= 1).all()
