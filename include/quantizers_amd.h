@@ -131,8 +131,9 @@ int qz_quantize_many(int64_t n, const void* const* w, void* const* q_out, void* 
  * drain (~3 us on MI355X) is paid once for the group instead of once per weight.  Replaces the
  * same per-module compressor loop as qz_quantize_many (do_oneshot.py:197).  `table` is a DEVICE
  * array of 4*n uint64 written by the caller before the launch (stream order):
- *   table[i] = weight i (bf16, dense, 16-B aligned), table[n+i] = its codes, table[2n+i] = its
- *   scales, table[3n+i] = its int8 zero points (required for asymmetric schemes, else 0).
+ *   table[i] = weight i (bf16, dense, 16-B aligned), table[n+i] = its codes (16-B aligned: the
+ *   kernels store 4- to 16-byte code words), table[2n+i] = its scales (2-B aligned),
+ *   table[3n+i] = its int8 zero points (required for asymmetric schemes, else 0).
  * Output layouts are exactly qz_quantize's with batch = 1.  No weight may alias any output.
  * Single-pass group schemes (GROUP / TENSOR_GROUP with a power-of-two group 8..512, int / FP8 /
  * MXFP4 / FP4, not NVFP4 and not fake-quant) and, from round 5, FP8_BLOCK 128 x 128 (e4m3 codes,

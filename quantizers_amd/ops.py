@@ -318,6 +318,8 @@ class GroupedQuantize:
         if len(outs) != len(ws):
             raise ValueError("GroupedQuantize: one output dict per weight")
         _check_no_alias(ws, outs)
+        if any(o["codes"].data_ptr() % 16 for o in outs):  # the table contract (quantizers_amd.h)
+            raise ValueError("GroupedQuantize: every codes output must be 16-B aligned")
         if not a.symmetric and any(o.get("zero_point") is None for o in outs):
             raise ValueError("GroupedQuantize: asymmetric schemes need a zero_point output per weight")
         n = len(ws)

@@ -1075,3 +1075,40 @@ def test_bench_config5_minimax_full_size(cuda):
         _eq(got["weight"], want["weight"])
         _eq(got["weight_scale"], want["weight_scale"])
     torch.cuda.empty_cache()
+
+
+def test_write_through_tail_gate_and_alignment(cuda):
+    """Round 6's write-through tail rules (qz_device.h wt_tail_from, qz_quant.hip encode_store):
+    a grouped int4 g128 launch writing >= 64 MiB of codes takes the tail, smaller launches do not,
+    and a table entry whose codes are only 4-B aligned keeps the 4-B stores inside a tail launch --
+    every case bit-identical to per-weight launches.  The misaligned table goes through the C ABI
+    (GroupedQuantize refuses codes that are not 16-B aligned, the header's contract)."""
+    import ctypes
+    from quantizers_amd import _lib
+    a = QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128)
+    r, c = 4096, 4096  # 8 MiB of codes per weight: 9 weights = 72 MiB (tail), 3 = 24 MiB (no tail)
+    ws = [_edge_weight(r, c, 128, seed=40 + s).to(cuda) for s in range(9)]
+    ref = [ops.quantize_weight(w, a) for w in ws]
+    for n in (3, 9):
+        got = ops.GroupedQuantize(ws[:n], a).run()
+        torch.cuda.synchronize()
+        for o, rf in zip(got, ref):
+            assert torch.equal(o["codes"], rf["codes"]) and torch.equal(o["scale"].view(torch.int16),
+                                                                         rf["scale"].view(torch.int16))
+    # codes of every other weight 4 bytes past a 16-B boundary
+    bufs = [torch.zeros(r * c // 8 + 4, dtype=torch.int32, device=cuda) for _ in ws]
+    codes = [b[1:].view(r, c // 8) if i % 2 else b[:-1].view(r, c // 8) for i, b in enumerate(bufs)]
+    scales = [torch.empty(r, c // 128, dtype=torch.bfloat16, device=cuda) for _ in ws]
+    assert all(codes[i].data_ptr() % 16 == 4 for i in range(1, 9, 2))
+    with pytest.raises(ValueError):
+        ops.GroupedQuantize(ws, a, outs=[{"codes": cd, "scale": sc, "zero_point": None}
+                                         for cd, sc in zip(codes, scales)])
+    table = torch.tensor([[w.data_ptr() for w in ws], [cd.data_ptr() for cd in codes],
+                          [sc.data_ptr() for sc in scales], [0] * 9], dtype=torch.int64).reshape(-1).to(cuda)
+    lib, ca = _lib.load(), a.to_c()
+    rc = lib.qz_quantize_grouped(9, ctypes.c_void_p(table.data_ptr()), r, c, ctypes.byref(ca),
+                                 _lib.QZ_OUT_PACKED_INT32, ops._stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    for cd, sc, rf in zip(codes, scales, ref):
+        assert torch.equal(cd, rf["codes"]) and torch.equal(sc.view(torch.int16), rf["scale"].view(torch.int16))
