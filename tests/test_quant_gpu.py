@@ -1096,8 +1096,9 @@ def test_write_through_tail_gate_and_alignment(cuda):
             assert torch.equal(o["codes"], rf["codes"]) and torch.equal(o["scale"].view(torch.int16),
                                                                          rf["scale"].view(torch.int16))
     # codes of every other weight 4 bytes past a 16-B boundary
-    bufs = [torch.zeros(r * c // 8 + 4, dtype=torch.int32, device=cuda) for _ in ws]
-    codes = [b[1:].view(r, c // 8) if i % 2 else b[:-1].view(r, c // 8) for i, b in enumerate(bufs)]
+    nw = r * c // 8
+    bufs = [torch.zeros(nw + 4, dtype=torch.int32, device=cuda) for _ in ws]
+    codes = [b[1:1 + nw].view(r, c // 8) if i % 2 else b[:nw].view(r, c // 8) for i, b in enumerate(bufs)]
     scales = [torch.empty(r, c // 128, dtype=torch.bfloat16, device=cuda) for _ in ws]
     assert all(codes[i].data_ptr() % 16 == 4 for i in range(1, 9, 2))
     with pytest.raises(ValueError):
