@@ -211,6 +211,12 @@ def oneshot(model: nn.Module, recipe: Union[str, dict, list], dataset=None, proc
     schemes = resolve_schemes(model, modifiers)
     if not schemes:
         raise ValueError("recipe targets no module of this model")
+    wrong = sorted({str(ref.weight.dtype) for ref in iter_linears(model)
+                    if ref.name in schemes and ref.weight.dtype != torch.bfloat16})
+    if wrong:  # every kernel reads bf16: fail before any work, not inside the AWQ pass or the save
+        raise ValueError(f"the MI355X kernels quantize bfloat16 weights (the reference loads its models in "
+                         f"bfloat16, scripts/do_oneshot.py:88); the recipe targets {', '.join(wrong)} weights: "
+                         f"load the model with torch_dtype=torch.bfloat16")
     report: Dict[str, Any] = {}
     layer_seconds: List[float] = []
     model.quantization_scheme_map = {n: s for n, (s, _) in schemes.items()}  # the residency plan reads it

@@ -659,6 +659,8 @@ def awq_weight_mean_accum(w: torch.Tensor, group_size: int, wsum: torch.Tensor) 
     """wsum[c] += sum_r |W[r,c]| / (group absmax + 1e-6) (fp64, deterministic: fixed-order
     reduction, ``awq_stats_layout``).  Returns rows added."""
     _check_dev(w, "weight")
+    if w.dtype != torch.bfloat16:  # the kernel reads bf16 weights (as every quantize kernel)
+        raise ValueError(f"awq_weight_mean_accum: weights must be bfloat16 (got {w.dtype})")
     w2 = w.reshape(-1, w.shape[-1])
     if w2.stride(-1) != 1:
         w2 = w2.contiguous()

@@ -790,6 +790,27 @@ def test_expert_w3_w2_awq_bf16_batched_statistics(cuda, calibrate_all):
         torch.testing.assert_close(torch.tensor(r["history"]), torch.tensor(hist), rtol=5e-3, atol=1e-12)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+def test_non_bf16_model_rejected_up_front(cuda, dtype):
+    """an fp16 / fp32 MoE model under the AWQ recipe.  Every kernel reads bf16 weights
+    (the reference loads bf16, do_oneshot.py:88), so oneshot refuses it before any work with a
+    ValueError that names the fix, instead of failing inside the expert searches or the save; the
+    statistics wrappers refuse non-bf16 weights too (awq_weight_mean_accum used to read them as
+    bf16), while activations of another dtype are converted (awq_absmean_accum, add_samples and the
+    expert searches' token runs)."""
+    m = _minimax(layers=1, experts=4).to(cuda, dtype)
+    with pytest.raises(ValueError, match="bfloat16"):
+        oneshot(m, os.path.join(ROOT, "configs/recipes/minimax_experts_awq.yaml"), dataset=_calib(vocab=256),
+                max_seq_length=64)
+    w = torch.randn(64, 256, device=cuda, dtype=dtype)
+    with pytest.raises(ValueError, match="bfloat16"):
+        ops.awq_weight_mean_accum(w, 32, torch.zeros(256, dtype=torch.float64, device=cuda))
+    x = torch.randn(40, 256, device=cuda, dtype=dtype)
+    s1, s2 = torch.zeros(256, device=cuda), torch.zeros(256, device=cuda)
+    assert ops.awq_absmean_accum(x, s1) == 40 and ops.awq_absmean_accum(x.to(torch.bfloat16), s2) == 40
+    assert torch.equal(s1, s2)
+
+
 def _awq_rank(rank, world, port, out):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
