@@ -74,3 +74,41 @@ def test_qparams_match_torch_ao_observers(bits, sym, strategy):
     assert torch.equal(fq_ct[same], fq_ao[same])
     assert (~same).float().mean() < 2e-3  # the quotient forms disagree only next to a rounding tie
     assert ((q_div - q_mul).abs() <= 1).all()
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+@pytest.mark.parametrize("sym", [True, False])
+@pytest.mark.parametrize("group", [32, 128, 0])
+def test_bf16_qparams_match_torch_affine_quantization(bits, sym, group):
+    """D3 in bf16: torch's affine quantization primitives (torch.ao.quantization.pt2e.
+    _affine_quantization._choose_qparams_affine, the torchao algorithm shipped in the image's torch)
+    evaluate the qparams in the weight's dtype (bf16 min / max, bf16 scale, zero point from a bf16
+    quotient), as the oracle restates compressed-tensors: group-wise (block [1, g]) and per-channel
+    (g = 0: block [1, cols]) scales are bit-identical on bf16 weights, int4 / int8, symmetric /
+    asymmetric, and so are the zero points except where compressed-tensors' extra bf16 rounding of
+    qmin - min / s (its op order) crosses a half-integer.  eps is passed as bf16's smallest normal, so torchao's clamp touches only
+    all-zero groups, which the data avoids (D1 / D10 differ there, see the module docstring)."""
+    from torch.ao.quantization.pt2e._affine_quantization import _choose_qparams_affine
+    w = _weights(seed=100 + bits + 2 * sym + group, rows=256, cols=2048).to(torch.bfloat16)
+    strategy = "group" if group else "channel"
+    a = ct.QArgs(num_bits=bits, type="int", symmetric=sym, strategy=strategy, group_size=group or None)
+    qmin, qmax = (int(v) for v in ct.calculate_range(a))
+    mn, mx = ct.observe_minmax(w, a)
+    s_ct, z_ct = ct.calculate_qparams(mn, mx, a)
+    s_ao, z_ao = _choose_qparams_affine(w, "SYMMETRIC" if sym else "ASYMMETRIC", [1, group or w.shape[1]],
+                                        torch.int8, qmin, qmax, eps=torch.finfo(torch.bfloat16).tiny)
+    assert s_ct.dtype == s_ao.dtype == torch.bfloat16
+    assert torch.equal(s_ct.reshape(-1).view(torch.int16), s_ao.reshape(-1).view(torch.int16)), "scales"
+    # zero points: torchao takes qmin - round(bf16(min / s)); compressed-tensors rounds
+    # bf16(qmin - bf16(min / s)), one more bf16 rounding -- they may differ only where that rounding
+    # moves the value across a half-integer (1 group in 16384 here)
+    if sym:
+        assert torch.equal(z_ct.reshape(-1).float(), z_ao.reshape(-1).float()), "zero points"
+        return
+    q = (torch.min(mn, torch.zeros_like(mn)) / s_ct).reshape(-1)
+    torchao_form = qmin - torch.round(q.float())
+    ct_form = torch.round((qmin - q).float())
+    same = torchao_form == ct_form
+    assert torch.equal(z_ct.reshape(-1).float()[same], z_ao.reshape(-1).float()[same]), "zero points"
+    assert torch.equal(z_ct.reshape(-1).float(), torch.clamp(ct_form, qmin, qmax))
+    assert (~same).sum() <= max(2, same.numel() // 1000)
