@@ -112,3 +112,22 @@ def test_bf16_qparams_match_torch_affine_quantization(bits, sym, group):
     assert torch.equal(z_ct.reshape(-1).float()[same], z_ao.reshape(-1).float()[same]), "zero points"
     assert torch.equal(z_ct.reshape(-1).float(), torch.clamp(ct_form, qmin, qmax))
     assert (~same).sum() <= max(2, same.numel() // 1000)
+
+
+@pytest.mark.parametrize("shape", ["group32", "group128", "channel", "block128"])
+def test_bf16_fp8_scales_match_torch_affine_quantization(shape):
+    """FP8-E4M3 scales (FP8 group / channel presets and FP8_BLOCK 128 x 128, the reference's mixed
+    and data-free recipes): torchao's symmetric float8 qparams (amax / ((qmax - qmin) / 2) with
+    qmax = 448, evaluated in bf16) equal the oracle's bf16 scales bit for bit."""
+    from torch.ao.quantization.pt2e._affine_quantization import _choose_qparams_affine
+    w = _weights(seed=200 + len(shape), rows=256, cols=2048).to(torch.bfloat16)
+    args = {"group32": dict(strategy="group", group_size=32), "group128": dict(strategy="group", group_size=128),
+            "channel": dict(strategy="channel"), "block128": dict(strategy="block", block_structure=(128, 128))}[shape]
+    block = {"group32": [1, 32], "group128": [1, 128], "channel": [1, 2048], "block128": [128, 128]}[shape]
+    a = ct.QArgs(num_bits=8, type="float", symmetric=True, **args)
+    mn, mx = ct.observe_minmax(w, a)
+    s_ct, _ = ct.calculate_qparams(mn, mx, a)
+    s_ao, _ = _choose_qparams_affine(w, "SYMMETRIC", block, torch.float8_e4m3fn,
+                                     eps=torch.finfo(torch.bfloat16).tiny)
+    assert s_ct.dtype == s_ao.dtype == torch.bfloat16
+    assert torch.equal(s_ct.reshape(-1).view(torch.int16), s_ao.reshape(-1).view(torch.int16))
