@@ -1113,3 +1113,37 @@ def test_write_through_tail_gate_and_alignment(cuda):
     torch.cuda.synchronize()
     for cd, sc, rf in zip(codes, scales, ref):
         assert torch.equal(cd, rf["codes"]) and torch.equal(sc.view(torch.int16), rf["scale"].view(torch.int16))
+
+
+@pytest.mark.parametrize("scheme", ["int4_g128_sym", "int4_g32_asym", "int8_channel_sym", "fp8_g32", "fp8_block128"])
+def test_kernel_scales_match_torch_affine_quantization(cuda, scheme):
+    """The kernels' bf16 scales (and int zero points) against torch's own quantization code directly
+    (torch.ao.quantization.pt2e._affine_quantization._choose_qparams_affine, torchao's algorithm;
+    the oracle-side pin is tests/test_torchao_pin.py): scales bit for bit; asymmetric zero points
+    equal wherever compressed-tensors' extra bf16 rounding of qmin - min / s does not cross a
+    half-integer."""
+    from torch.ao.quantization.pt2e._affine_quantization import _choose_qparams_affine
+    a, block, tdt = {
+        "int4_g128_sym": (QuantizationArgs(num_bits=4, type="int", symmetric=True, group_size=128), [1, 128], torch.int8),
+        "int4_g32_asym": (QuantizationArgs(num_bits=4, type="int", symmetric=False, group_size=32), [1, 32], torch.int8),
+        "int8_channel_sym": (QuantizationArgs(num_bits=8, type="int", symmetric=True, strategy="channel"), [1, 2048],
+                             torch.int8),
+        "fp8_g32": (QuantizationArgs(num_bits=8, type="float", symmetric=True, group_size=32), [1, 32],
+                    torch.float8_e4m3fn),
+        "fp8_block128": (QuantizationArgs(**FP8_BLOCK), [128, 128], torch.float8_e4m3fn)}[scheme]
+    g = torch.Generator().manual_seed(77)
+    w = (torch.randn(512, 2048, generator=g) * (torch.rand(512, 1, generator=g) * 0.05 + 1e-3)).to(torch.bfloat16)
+    got = ops.quantize_weight(w.to(cuda), a)
+    torch.cuda.synchronize()
+    qmin, qmax = (-8, 7) if a.num_bits == 4 else (-128, 127)
+    kw = {} if tdt == torch.float8_e4m3fn else {"quant_min": qmin, "quant_max": qmax}
+    s_ao, z_ao = _choose_qparams_affine(w, "SYMMETRIC" if a.symmetric else "ASYMMETRIC", block, tdt,
+                                        eps=torch.finfo(torch.bfloat16).tiny, **kw)
+    assert torch.equal(got["scale"].cpu().reshape(-1).view(torch.int16), s_ao.reshape(-1).view(torch.int16))
+    if not a.symmetric:
+        zp = got["zero_point"].cpu().reshape(-1).float()
+        mn = torch.min(w.reshape(-1, block[1]).amin(-1), torch.zeros(1, dtype=torch.bfloat16))
+        q = mn / s_ao.reshape(-1)
+        same = (qmin - torch.round(q.float())) == torch.round((qmin - q).float())
+        assert torch.equal(zp[same], z_ao.reshape(-1).float()[same])
+        assert (~same).sum() <= max(2, same.numel() // 1000)
