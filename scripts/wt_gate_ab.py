@@ -61,10 +61,20 @@ def main(paths):
     seq = open(seq_path, "w") if seq_path else None
     steps = int(os.environ.get("K", 10))
 
+    # one-entry grouped tables (register loads, GRP kernel) per weight, into the same 100 outputs
+    tabs = [torch.tensor([[ws[i].data_ptr()], [outs[i]["codes"].data_ptr()], [outs[i]["scale"].data_ptr()], [0]],
+                         dtype=torch.int64).reshape(-1).to(dev) for i in range(k)]
+    tab_ptrs = [P(t.data_ptr()) for t in tabs]
     one = [P(outs[0]["codes"].data_ptr())] * k, [P(outs[0]["scale"].data_ptr())] * k
     q1_arr, s1_arr = (P * k)(*one[0]), (P * k)(*one[1])
 
     def leg(lib, name, reps=1):
+        if name == "pw_grp":  # one-weight launches of the grouped (register-load) kernel
+            for _ in range(reps):
+                for tp in tab_ptrs:
+                    rc = lib.qz_quantize_grouped(1, tp, R, C, ctypes.byref(gq.ca), gq.out_fmt, sp)
+                    assert rc == 0, rc
+            return k * reps
         if name == "pw_same":  # scripts/kernel_driver.py's pattern: every launch into ONE output set
             for _ in range(reps):
                 rc = lib.qz_quantize_many(k, w_arr, q1_arr, s1_arr, None, None, 1, R, C, C, R * C, ctypes.byref(ca),
@@ -106,10 +116,11 @@ def main(paths):
             print(f"{os.path.basename(p)}: outputs {'identical' if all(torch.equal(x, y) for x, y in zip(base, got)) else 'MISMATCH'}",
                   flush=True)
     rounds = int(os.environ.get("ROUNDS", 7))
-    res = {(p, l): [] for p in paths for l in ("per_weight", "pw_same", "grouped", "plan")}
+    legs = os.environ.get("LEGS", "per_weight,pw_same,grouped,plan").split(",")
+    res = {(p, l): [] for p in paths for l in legs}
     for _ in range(rounds):
         for p, lib in zip(paths, libs):
-            for name, reps in (("per_weight", 1), ("pw_same", 1), ("grouped", 3), ("plan", steps)):
+            for name, reps in [(l, {"grouped": 3, "plan": steps}.get(l, 1)) for l in legs]:
                 n = leg(lib, name, 1 if name != "plan" else 2)  # warm: the same pattern once
                 if seq:
                     seq.write(f"{os.path.basename(p)} warm {n}\n")
@@ -120,9 +131,12 @@ def main(paths):
                 torch.cuda.synchronize()
                 if seq:
                     seq.write(f"{os.path.basename(p)} {name} {n}\n")
-                per = {"per_weight": k, "pw_same": k, "grouped": k * reps, "plan": reps}[name]
+                per = {"per_weight": k, "pw_same": k, "pw_grp": k, "grouped": k * reps, "plan": reps}[name]
                 res[(p, name)].append(e0.elapsed_time(e1) * 1e3 / per)
-    for name, unit in (("per_weight", "us/launch"), ("pw_same", "us/launch"), ("grouped", "us/weight"), ("plan", "us/step")):
+    for name, unit in (("per_weight", "us/launch"), ("pw_same", "us/launch"), ("pw_grp", "us/launch"),
+                       ("grouped", "us/weight"), ("plan", "us/step")):
+        if name not in legs:
+            continue
         for p in paths:
             v = sorted(res[(p, name)])
             print(f"{name:11s} {os.path.basename(p):18s} event median {v[len(v) // 2]:9.2f} {unit}  min {v[0]:9.2f}",

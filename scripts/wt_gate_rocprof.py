@@ -25,19 +25,25 @@ def main(trace, seq_path):
     by = defaultdict(list)
     for lib, leg, n in blocks:
         n = int(n)
-        if leg in ("per_weight", "pw_same", "grouped", "plan"):
+        if leg in ("per_weight", "pw_same", "pw_grp", "grouped", "plan"):
             by[(lib, leg)].append(durs[pos:pos + n])
         pos += n
     libs = sorted({lib for lib, _ in by}, key=[b[0] for b in blocks].index)
-    for lib, leg in [(x, y) for y in ("per_weight", "pw_same") for x in libs]:
+    for lib, leg in [(x, y) for y in ("per_weight", "pw_same", "pw_grp") for x in libs]:
         pw = [d for blk in by[(lib, leg)] for d in blk]
+        if not pw:
+            continue
         print(f"{leg:10s} {lib:18s} rocprof median {statistics.median(pw):8.2f} us/launch  n={len(pw)}  "
               f"frac {113426432 / (statistics.median(pw) * 1e-6) / 8e12:.3f}")
     for lib in libs:
         gr = [d / 100 for blk in by[(lib, "grouped")] for d in blk]
+        if not gr:
+            continue
         print(f"grouped    {lib:18s} rocprof median {statistics.median(gr):8.2f} us/weight  n={len(gr)}")
     for lib in libs:
         steps = [blk[i:i + 5] for blk in by[(lib, "plan")] for i in range(0, len(blk), 5)]
+        if not steps:
+            continue
         per = [statistics.median(s[j] for s in steps) for j in range(5)]
         print(f"plan       {lib:18s} rocprof median step {statistics.median(sum(s) for s in steps):8.2f} us  "
               f"launches " + " ".join(f"{v:.2f}" for v in per) + f"  steps={len(steps)}")
