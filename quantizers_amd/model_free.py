@@ -252,28 +252,35 @@ def model_free_ptq(model_stub: str, save_directory: str, scheme: Union[str, Quan
             targets, mods, sk = _select(hdr[1], sch, ignore)
             return path, hdr, targets, mods, sk, stager.load(path, targets, hdr)
 
-        pending = [enqueue(f) for f in mine[:LOOKAHEAD]]
+        pending = []
         writes = []
-        for i, fn in enumerate(mine):
-            path, hdr, targets, mods, sk, fl = pending[i]
-            pending[i] = None
-            if i + LOOKAHEAD < len(mine):
-                pending.append(enqueue(mine[i + LOOKAHEAD]))
-            t_wait = time.perf_counter()
-            dev = stager.wait(fl)  # the quantize launches (current stream) see the loaded weights
-            _span("read_wait", t_wait, fl.nbytes)  # the main thread blocked on this file's reads + DMAs
-            out = _rest(path, hdr[1], targets)
-            out.update(_quantize_file([dev[n] for n in targets], mods, sch, device, copier))
-            del dev, fl
-            quantized.extend(mods)
-            skipped.extend(sk)
-            ready = copier.last_event
-            for k, t in out.items():
-                weight_map[k] = fn
-                total += t.numel() * t.element_size()
-            writes.append(wpool.submit(_write_shard, out, os.path.join(save_directory, fn), ready))
-        for w in writes:
-            w.result()
+        try:
+            for f in mine[:LOOKAHEAD]:
+                pending.append(enqueue(f))
+            for i, fn in enumerate(mine):
+                path, hdr, targets, mods, sk, fl = pending[i]
+                pending[i] = None
+                if i + LOOKAHEAD < len(mine):
+                    pending.append(enqueue(mine[i + LOOKAHEAD]))
+                t_wait = time.perf_counter()
+                dev = stager.wait(fl)  # the quantize launches (current stream) see the loaded weights
+                _span("read_wait", t_wait, fl.nbytes)  # the main thread blocked on this file's reads + DMAs
+                out = _rest(path, hdr[1], targets)
+                out.update(_quantize_file([dev[n] for n in targets], mods, sch, device, copier))
+                del dev, fl
+                quantized.extend(mods)
+                skipped.extend(sk)
+                ready = copier.last_event
+                for k, t in out.items():
+                    weight_map[k] = fn
+                    total += t.numel() * t.element_size()
+                writes.append(wpool.submit(_write_shard, out, os.path.join(save_directory, fn), ready))
+            for w in writes:
+                w.result()
+        finally:  # on an error: the files queued ahead are closed once their reads can no longer run
+            for p in pending:
+                if p is not None:
+                    stager.release(p[5])
         copier.finish()
     torch.cuda.synchronize(device)
     LAST_RUN["wall"] = time.perf_counter() - t_call

@@ -182,8 +182,22 @@ class DiskStager:
             for f in fl.futures:
                 f.result()
         finally:
-            os.close(fl.fd)
+            self.release(fl)
         ev = torch.cuda.Event()
         ev.record(self.stream)
         (stream if stream is not None else torch.cuda.current_stream(self.device)).wait_event(ev)
         return fl.tensors
+
+    @staticmethod
+    def release(fl: FileLoad) -> None:
+        """Close ``fl``'s file once none of its reads can still run (a failed or abandoned load:
+        its other chunks finish or fail first, so no read ever lands on a reused descriptor)."""
+        if fl.fd < 0:
+            return
+        for f in fl.futures:
+            f.cancel()
+        for f in fl.futures:
+            if not f.cancelled():
+                f.exception()  # waits; the error, if any, is the caller's to report
+        os.close(fl.fd)
+        fl.fd = -1

@@ -127,3 +127,35 @@ def test_model_free_two_ranks(cuda, tmp_path):
         _eq(two[k], one[k], k)
     for f in ("config.json", "model.safetensors.index.json"):
         assert json.load(open(tmp_path / "one" / f)) == json.load(open(tmp_path / "two" / f))
+
+
+def test_model_free_torn_shard_raises_and_closes(cuda, tmp_path):
+    """A shard shorter than its header says (a torn download) stops the call with the short read,
+    and every input file is closed afterwards -- the failing one and those queued ahead of it."""
+    g = torch.Generator().manual_seed(2)
+    src = tmp_path / "src"
+    os.makedirs(src)
+    names = [f"model-{i + 1:05d}-of-00004.safetensors" for i in range(4)]
+    wmap = {}
+    for i, fn in enumerate(names):
+        save_file({f"l{i}.{p}.weight": (torch.randn(128, 256, generator=g) * 0.02).to(torch.bfloat16)
+                   for p in ("q", "k")}, str(src / fn))
+        wmap.update({f"l{i}.{p}.weight": fn for p in ("q", "k")})
+    (src / "model.safetensors.index.json").write_text(json.dumps({"metadata": {}, "weight_map": wmap}))
+    os.truncate(src / names[0], os.path.getsize(src / names[0]) - 4096)
+    with pytest.raises(IOError, match="short read"):
+        model_free_ptq(str(src), str(tmp_path / "dst"), scheme="W4A16", max_workers=4, device=cuda)
+    assert _open_under(src) == []
+
+
+def _open_under(d):
+    """This process's open file descriptors on files under directory ``d``."""
+    out = []
+    for fd in os.listdir("/proc/self/fd"):
+        try:
+            t = os.readlink(f"/proc/self/fd/{fd}")
+        except OSError:
+            continue
+        if t.startswith(str(d) + os.sep):
+            out.append(t)
+    return out

@@ -72,3 +72,46 @@ def test_disk_stager_loads_every_byte(cuda, tmp_path, slots, slot_bytes):
                 assert dev[k].dtype == t[k].dtype and dev[k].shape == t[k].shape
                 assert torch.equal(dev[k].cpu().reshape(-1).view(torch.uint8), t[k].reshape(-1).view(torch.uint8)), k
                 assert sums[k].item() == t[k].double().sum().item()
+
+
+def test_disk_stager_truncated_file_fails_and_closes(cuda, tmp_path):
+    """A file shorter than its header says (a torn copy): ``wait`` raises the short read, and the
+    file is closed only after every other chunk of the load has finished -- also for a load that is
+    released without being waited on (model_free_ptq's files queued ahead of a failure)."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+    from safetensors.torch import save_file
+    from quantizers_amd.staging import DiskStager, safetensors_header
+    g = torch.Generator().manual_seed(7)
+    p = str(tmp_path / "torn.safetensors")
+    save_file({"a.weight": torch.randn(64, 256, generator=g).to(torch.bfloat16),
+               "b.weight": torch.randn(64, 256, generator=g).to(torch.bfloat16)}, p)
+    hdr = safetensors_header(p)
+    os.truncate(p, os.path.getsize(p) - 1000)
+
+    def fds():  # open descriptors on the torn file
+        n = 0
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                n += os.readlink(f"/proc/self/fd/{fd}") == p
+            except OSError:
+                pass
+        return n
+    with ThreadPoolExecutor(max_workers=4) as pool:
+        st = DiskStager(cuda, pool, slots=2, slot_bytes=4096)
+        assert fds() == 0
+        fl = st.load(p, ["a.weight", "b.weight"], hdr)
+        with pytest.raises(IOError, match="short read"):
+            st.wait(fl)
+        assert fl.fd == -1 and all(f.done() for f in fl.futures) and fds() == 0
+        fl2 = st.load(p, ["a.weight", "b.weight"], hdr)
+        st.release(fl2)
+        assert fl2.fd == -1 and all(f.done() for f in fl2.futures) and fds() == 0
+        st.release(fl2)  # idempotent
+        # the stager keeps working after a failed load
+        good = str(tmp_path / "good.safetensors")
+        w = torch.randn(33, 65, generator=g).to(torch.bfloat16)
+        save_file({"w.weight": w}, good)
+        dev = st.wait(st.load(good, ["w.weight"]))
+        torch.cuda.synchronize()
+        assert torch.equal(dev["w.weight"].cpu().view(torch.int16), w.view(torch.int16))
