@@ -45,20 +45,32 @@ def main():
         assert rc == 0, rc
 
     nb = lib.qzp_gemm_sqerr_tiles(T, N)
+    parts = lambda m: nb * 8 if m & 64 else nb  # noqa: E731  (the persistent form: 8 partials per tile)
     # 1. exact layout check, both orientations
     xi = torch.randint(-3, 4, (T, K), device=dev, generator=g).to(torch.bfloat16)
     wi = torch.randint(-3, 4, (N, K), device=dev, generator=g).to(torch.bfloat16)
     ci = torch.empty(T, N, dtype=torch.bfloat16, device=dev)
     ref = (xi.float() @ wi.float().t()).to(torch.bfloat16)
-    for mode in (0, 2, 4, 6, 8, 16):
+    env_modes = lambda k, d: [int(v) for v in os.environ.get(k, d).split(",")]  # noqa: E731
+    for mode in env_modes("LAYOUT_MODES", "0,2,4,6,8,16"):
         ci.zero_()
-        tab, _ = table([(xi, wi, ci, T)], nb)
+        tab, _ = table([(xi, wi, ci, T)], parts(mode))
         launch(tab, 1, T, ci, mode)
         exact = torch.equal(ci.view(torch.int16), ref.view(torch.int16))
         print(f"layout check mode {mode} (exact integer data): {'OK' if exact else 'MISMATCH'}", flush=True)
         if not exact:
             print("first mismatches", (ci.float() != ref.float()).nonzero()[:5].tolist(), flush=True)
             return
+        reps = int(os.environ.get("RACE_REPS", 0))  # race screen: the same launch again and again
+        if reps and mode & 96:
+            bad = 0
+            for _ in range(reps):
+                ci.zero_()
+                launch(tab, 1, T, ci, mode)
+                bad += int(not torch.equal(ci.view(torch.int16), ref.view(torch.int16)))
+            print(f"  race screen mode {mode}: {bad} of {reps} launches differ", flush=True)
+            if bad:
+                return
     del xi, wi, ci, ref
     # 2. losses
     x = torch.randn(T, K, device=dev, generator=g).to(torch.bfloat16)
@@ -71,19 +83,19 @@ def main():
         acc = torch.zeros(1, dtype=torch.float64, device=dev)
         ops.awq_sq_err_accum(torch.nn.functional.linear(x_, w_), r_.contiguous(), acc)
         return acc.item()
-    for mode in (7, 17):
-        tab, part = table([(x, ws[0], r, T)], nb)
+    for mode in env_modes("LOSS_MODES", "7,17"):
+        tab, part = table([(x, ws[0], r, T)], parts(mode))
         launch(tab, 1, T, None, mode)
         torch.cuda.synchronize()
         lf, lr = part.sum().item(), ref_loss(x, ws[0], r)
         print(f"loss mode {mode}: fused {lf:.9e} product {lr:.9e} rel {(lf - lr) / lr:.2e}", flush=True)
         for tr in (1000, 4097, 300):  # ragged rows
-            tab, part = table([(x, ws[1], r, tr)], nb)
+            tab, part = table([(x, ws[1], r, tr)], parts(mode))
             launch(tab, 1, T, None, mode)
             torch.cuda.synchronize()
             lf, lr = part.sum().item(), ref_loss(x[:tr], ws[1], r[:tr])
             print(f"  ragged rows {tr}: fused {lf:.9e} product {lr:.9e} rel {(lf - lr) / lr:.2e}", flush=True)
-        tab, part = table([(x, wq, r, T) for wq in ws], nb)
+        tab, part = table([(x, wq, r, T) for wq in ws], parts(mode))
         launch(tab, 8, T, None, mode)
         torch.cuda.synchronize()
         rel = max(abs(part[i].sum().item() / ref_loss(x, ws[i], r) - 1) for i in range(8))
@@ -125,14 +137,15 @@ def main():
     us_mm = t_of(lambda: torch.mm(xs[0], ws[0].t(), out=outs[0]), 1)
     print(f"{'  of which hipBLASLt mm':40s} {us_mm:9.2f} us  {flop / (us_mm * 1e-6) / 1e15:.3f} PFLOP/s", flush=True)
     cbuf = torch.empty_like(rs[0])
-    for mode in (6, 16, 7, 17):
-        tab1, _ = table([(xs[0], ws[0], rs[0] if mode & 1 else cbuf, T)], nb)
+    for mode in env_modes("TIME_MODES", "6,16,7,17"):
+        tab1, _ = table([(xs[0], ws[0], rs[0] if mode & 1 else cbuf, T)], parts(mode))
         us1 = t_of(lambda: launch(tab1, 1, T, cbuf, mode), 1)
         line = f"mode {mode} ({'fused loss' if mode & 1 else 'core, bf16 store'}, BK {64 if mode & 28 else 32}" \
-               f"{', 4 waves' if mode & 8 else ''}{', 4 waves pipelined' if mode & 16 else ''}): one item " \
+               f"{', 4 waves' if mode & 8 else ''}{', 4 waves pipelined' if mode & 16 else ''}" \
+               f"{', staggered phases' if mode & 32 else ''}{', persistent staggered' if mode & 64 else ''}): one item " \
                f"{us1:9.2f} us ({flop / (us1 * 1e-6) / 1e15:.3f} PFLOP/s)"
         if mode & 1:
-            tabn, partn = table([(xs[k], wq_all[j, k], rs[k], T) for k in range(E) for j in range(8)], nb)
+            tabn, partn = table([(xs[k], wq_all[j, k], rs[k], T) for k in range(E) for j in range(8)], parts(mode))
             usn = t_of(lambda: launch(tabn, 8 * E, T, None, mode), 8 * E)
             line += f", {8 * E} items per launch {usn:9.2f} us per grid point ({flop / (usn * 1e-6) / 1e15:.3f} PFLOP/s)"
         print(line, flush=True)
